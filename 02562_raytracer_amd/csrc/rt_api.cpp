@@ -1,0 +1,663 @@
+// rt_api.cpp -- the extern "C" boundary (include/rt.h): HIP device/stream
+// wrapper (replaces src/gpu_handles.rs), storage-buffer uploads (replaces
+// src/bindings/*.rs create_buffer_init) with the MI355X data layout repack,
+// and RenderState::render (src/render_state.rs:483-561).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "host_types.h"
+#include "rt_internal.h"
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { reset(); }
+    void reset()
+    {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+    }
+    hipError_t alloc(size_t bytes)
+    {
+        reset();
+        if (bytes == 0) bytes = 16;
+        hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return e;
+        }
+        n = bytes;
+        return hipSuccess;
+    }
+    template <class T>
+    T* as() const
+    {
+        return reinterpret_cast<T*>(p);
+    }
+};
+
+}  // namespace
+
+struct rt_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    std::string err;
+    int num_cus = 256;
+    int waves_per_cu = 16;
+    bool detail = false;
+    // host copies needed to build the triangle records on BSP/BVH upload
+    std::vector<float> h_pos;
+    std::vector<uint32_t> h_idx;
+    uint32_t nverts = 0, ntris = 0, nmats = 0, nlights = 0;
+    bool has_mesh = false;
+    DevBuf pos, nrm, idx, mats, lights;
+    DevBuf bsp_nodes, bsp_recs, bsp_ids;
+    uint32_t bsp_depth = 0;
+    float aabb[6] = {0, 0, 0, 0, 0, 0};
+    bool has_bsp = false;
+    DevBuf bvh_nodes, bvh_recs, bvh_ids;
+    uint32_t bvh_nnodes = 0;
+    bool has_bvh = false;
+    rt_uniform u;
+    bool has_u = false;
+    DevBuf jitter;
+    bool has_jitter = false;
+    float env[3] = {1.0f, 1.0f, 1.0f};
+    DevBuf work, counters;
+    rt_ray_counts last;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+int fail(rt_ctx* c, int code, const std::string& msg)
+{
+    if (c) c->err = msg;
+    else rthost::set_error(msg);
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? RT_E_OOM : RT_E_DEVICE,                   \
+                        std::string(#expr ": ") + hipGetErrorString(e_));                          \
+    } while (0)
+
+int upload(rt_ctx* c, DevBuf& b, const void* src, size_t bytes)
+{
+    hipError_t e = b.alloc(bytes);
+    if (e != hipSuccess)
+        return fail(c, e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_DEVICE,
+                    std::string("hipMalloc: ") + hipGetErrorString(e));
+    if (bytes) HIPCHK(c, hipMemcpy(b.p, src, bytes, hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+// 48-byte triangle record {v0, e0 = v1 - v0, e1 = v2 - v0, n = cross(e0, e1)}
+// for every slot of `ids` (IEEE f32, no contraction: identical to computing
+// them per test in the shader).
+void build_recs(const std::vector<float>& pos, const std::vector<uint32_t>& idx, const uint32_t* ids, size_t nids,
+                std::vector<float>& out)
+{
+    out.resize(nids * 12);
+    auto work = [&](size_t lo, size_t hi) {
+        for (size_t k = lo; k < hi; k++) {
+            const uint32_t* ix = &idx[(size_t)ids[k] * 4];
+            const float* a = &pos[(size_t)ix[0] * 4];
+            const float* b = &pos[(size_t)ix[1] * 4];
+            const float* c = &pos[(size_t)ix[2] * 4];
+            const float e0[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+            const float e1[3] = {c[0] - a[0], c[1] - a[1], c[2] - a[2]};
+            const float n[3] = {e0[1] * e1[2] - e0[2] * e1[1], e0[2] * e1[0] - e0[0] * e1[2],
+                                e0[0] * e1[1] - e0[1] * e1[0]};
+            float* o = &out[k * 12];
+            o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = e0[0];
+            o[4] = e0[1]; o[5] = e0[2]; o[6] = e1[0]; o[7] = e1[1];
+            o[8] = e1[2]; o[9] = n[0]; o[10] = n[1]; o[11] = n[2];
+        }
+    };
+    const size_t nthr = std::min<size_t>(std::max(1u, std::thread::hardware_concurrency()), 32);
+    if (nids < 65536 || nthr == 1) {
+        work(0, nids);
+        return;
+    }
+    std::vector<std::thread> th;
+    const size_t chunk = (nids + nthr - 1) / nthr;
+    for (size_t t = 0; t < nthr; t++) {
+        const size_t lo = t * chunk, hi = std::min(nids, lo + chunk);
+        if (lo < hi) th.emplace_back(work, lo, hi);
+    }
+    for (auto& t : th) t.join();
+}
+
+int set_dev(rt_ctx* c)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    return RT_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rt_device_count(int* count)
+{
+    if (!count) return fail(nullptr, RT_E_INVALID, "rt_device_count: null");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) {
+        *count = 0;
+        return fail(nullptr, RT_E_DEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *count = n;
+    return RT_OK;
+}
+
+int rt_create(int device, rt_ctx** out)
+{
+    if (!out) return fail(nullptr, RT_E_INVALID, "rt_create: null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(nullptr, RT_E_DEVICE, "rt_create: no such HIP device");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess)
+        return fail(nullptr, RT_E_DEVICE, "rt_create: hipGetDeviceProperties failed");
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(nullptr, RT_E_DEVICE, std::string("rt_create: kernels are built for gfx950, device is ") +
+                                              prop.gcnArchName);
+    rt_ctx* c = new rt_ctx();
+    c->device = device;
+    c->num_cus = prop.multiProcessorCount;
+    memset(&c->u, 0, sizeof c->u);
+    memset(&c->last, 0, sizeof c->last);
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
+        c->work.alloc(64) != hipSuccess || c->counters.alloc(16 * sizeof(unsigned long long)) != hipSuccess) {
+        delete c;
+        return fail(nullptr, RT_E_DEVICE, "rt_create: stream/buffer setup failed");
+    }
+    c->stream = c->own;
+    *out = c;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipDeviceSynchronize();
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int rt_set_stream(rt_ctx* c, void* s)
+{
+    if (!c) return RT_E_INVALID;
+    c->stream = s ? (hipStream_t)s : c->own;
+    return RT_OK;
+}
+
+void* rt_get_stream(rt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
+int rt_synchronize(rt_ctx* c)
+{
+    if (!c) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_set_option(rt_ctx* c, int option, int64_t value)
+{
+    if (!c) return RT_E_INVALID;
+    switch (option) {
+    case RT_OPT_DETAIL_COUNTERS:
+        c->detail = value != 0;
+        return RT_OK;
+    case RT_OPT_WAVES_PER_CU:
+        if (value < 1 || value > 32) return fail(c, RT_E_INVALID, "waves per CU must be in [1,32]");
+        c->waves_per_cu = (int)value;
+        return RT_OK;
+    default:
+        return fail(c, RT_E_INVALID, "unknown option");
+    }
+}
+
+const char* rt_last_error(const rt_ctx* c) { return c ? c->err.c_str() : rthost::get_error(); }
+
+int rt_device_alloc(rt_ctx* c, size_t bytes, void** dptr)
+{
+    if (!c || !dptr) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    *dptr = nullptr;
+    HIPCHK(c, hipMalloc(dptr, bytes ? bytes : 16));
+    return RT_OK;
+}
+
+int rt_device_free(rt_ctx* c, void* dptr)
+{
+    if (!c) return RT_E_INVALID;
+    if (!dptr) return RT_OK;
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, hipFree(dptr));
+    return RT_OK;
+}
+
+int rt_memcpy_to_host(rt_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c || (!dst && bytes) || (!src && bytes)) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_memcpy_to_device(rt_ctx* c, void* dst, const void* src, size_t bytes)
+{
+    if (!c || (!dst && bytes) || (!src && bytes)) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_memset_device(rt_ctx* c, void* dst, int value, size_t bytes)
+{
+    if (!c || (!dst && bytes)) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipMemsetAsync(dst, value, bytes, c->stream));
+    return RT_OK;
+}
+
+int rt_timer_start(rt_ctx* c)
+{
+    if (!c) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    if (!c->ev0) {
+        HIPCHK(c, hipEventCreate(&c->ev0));
+        HIPCHK(c, hipEventCreate(&c->ev1));
+    }
+    HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    return RT_OK;
+}
+
+int rt_timer_stop(rt_ctx* c, float* ms)
+{
+    if (!c || !ms || !c->ev0) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipEventRecord(c->ev1, c->stream));
+    HIPCHK(c, hipEventSynchronize(c->ev1));
+    HIPCHK(c, hipEventElapsedTime(ms, c->ev0, c->ev1));
+    return RT_OK;
+}
+
+int rt_upload_mesh(rt_ctx* c, const float* pos_vec4, const float* nrm_vec4, uint32_t nverts,
+                   const uint32_t* idx_vec4u, uint32_t ntris, const rt_material* mats, uint32_t nmats,
+                   const uint32_t* light_idx, uint32_t nlight)
+{
+    if (!c) return RT_E_INVALID;
+    if ((!pos_vec4 && nverts) || (!idx_vec4u && ntris) || !mats || nmats == 0)
+        return fail(c, RT_E_INVALID, "rt_upload_mesh: missing arrays (need >= 1 material)");
+    for (size_t t = 0; t < ntris; t++)
+        for (int k = 0; k < 3; k++)
+            if (idx_vec4u[t * 4 + k] >= nverts) return fail(c, RT_E_INVALID, "rt_upload_mesh: vertex index out of range");
+    std::vector<uint32_t> lights;
+    if (light_idx) {
+        if (nlight == 0 || light_idx[0] != 0xFFFFFFFFu)
+            return fail(c, RT_E_INVALID, "rt_upload_mesh: light list must start with the UINT32_MAX sentinel");
+        lights.assign(light_idx, light_idx + nlight);
+        for (uint32_t i = 1; i < nlight; i++)
+            if (lights[i] >= ntris) return fail(c, RT_E_INVALID, "rt_upload_mesh: light index out of range");
+    } else {
+        std::vector<uint32_t> ix(idx_vec4u, idx_vec4u + (size_t)ntris * 4);
+        std::vector<rt_material> mv(mats, mats + nmats);
+        lights = rthost::light_list(ix, mv);
+    }
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_mesh = c->has_bsp = c->has_bvh = false;
+    c->h_pos.assign(pos_vec4, pos_vec4 + (size_t)nverts * 4);
+    c->h_idx.assign(idx_vec4u, idx_vec4u + (size_t)ntris * 4);
+    std::vector<float> nrm;
+    if (nrm_vec4) nrm.assign(nrm_vec4, nrm_vec4 + (size_t)nverts * 4);
+    else nrm.assign((size_t)nverts * 4, 0.0f);
+    int r;
+    if ((r = upload(c, c->pos, c->h_pos.data(), c->h_pos.size() * 4))) return r;
+    if ((r = upload(c, c->nrm, nrm.data(), nrm.size() * 4))) return r;
+    if ((r = upload(c, c->idx, c->h_idx.data(), c->h_idx.size() * 4))) return r;
+    if ((r = upload(c, c->mats, mats, (size_t)nmats * sizeof(rt_material)))) return r;
+    if ((r = upload(c, c->lights, lights.data(), lights.size() * 4))) return r;
+    c->nverts = nverts;
+    c->ntris = ntris;
+    c->nmats = nmats;
+    c->nlights = (uint32_t)lights.size();
+    c->has_mesh = true;
+    return RT_OK;
+}
+
+int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const float* planes, uint32_t nnodes,
+                  const uint32_t* ids, uint32_t nids, uint32_t max_depth)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_upload_bsp: upload the mesh first");
+    if (!aabb || !tree || !planes || (!ids && nids)) return fail(c, RT_E_INVALID, "rt_upload_bsp: null array");
+    if (max_depth == 0 || max_depth >= 32 || (uint64_t)nnodes != ((uint64_t)1 << (max_depth + 1)) - 1)
+        return fail(c, RT_E_INVALID, "rt_upload_bsp: nnodes must be 2^(max_depth+1)-1, max_depth in [1,31]");
+    for (uint32_t k = 0; k < nids; k++)
+        if (ids[k] >= c->ntris) return fail(c, RT_E_INVALID, "rt_upload_bsp: triangle id out of range");
+    // validate the reachable tree (implicit children, leaves inside ids)
+    std::vector<uint32_t> stack{0};
+    std::vector<uint32_t> packed((size_t)nnodes * 2, 0u);
+    for (uint32_t i = 0; i < nnodes; i++) {
+        packed[2 * (size_t)i] = tree[4 * (size_t)i];
+        uint32_t pbits;
+        memcpy(&pbits, &planes[i], 4);
+        packed[2 * (size_t)i + 1] = (tree[4 * (size_t)i] & 3u) == 3u ? tree[4 * (size_t)i + 1] : pbits;
+    }
+    while (!stack.empty()) {
+        const uint32_t i = stack.back();
+        stack.pop_back();
+        const uint32_t* n = tree + 4 * (size_t)i;
+        if ((n[0] & 3u) == 3u) {
+            if ((uint64_t)n[1] + (n[0] >> 2) > nids)
+                return fail(c, RT_E_INVALID, "rt_upload_bsp: leaf range outside treeIds");
+            continue;
+        }
+        const uint64_t l = 2ull * i + 1, rgt = 2ull * i + 2;
+        if (rgt >= nnodes || n[2] != l || n[3] != rgt)
+            return fail(c, RT_E_INVALID, "rt_upload_bsp: interior node children are not 2i+1, 2i+2 inside the array");
+        stack.push_back((uint32_t)l);
+        stack.push_back((uint32_t)rgt);
+    }
+    std::vector<float> recs;
+    build_recs(c->h_pos, c->h_idx, ids, nids, recs);
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_bsp = false;
+    int r;
+    if ((r = upload(c, c->bsp_nodes, packed.data(), packed.size() * 4))) return r;
+    if ((r = upload(c, c->bsp_recs, recs.data(), recs.size() * 4))) return r;
+    if ((r = upload(c, c->bsp_ids, ids, (size_t)nids * 4))) return r;
+    c->bsp_depth = max_depth;
+    c->aabb[0] = aabb[0];
+    c->aabb[1] = aabb[1];
+    c->aabb[2] = aabb[2];
+    c->aabb[3] = aabb[4];
+    c->aabb[4] = aabb[5];
+    c->aabb[5] = aabb[6];
+    c->has_bsp = true;
+    return RT_OK;
+}
+
+int rt_upload_bvh(rt_ctx* c, const rt_gpu_node* nodes, uint32_t nnodes, const uint32_t* tri_ids, uint32_t nids)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_upload_bvh: upload the mesh first");
+    if (!nodes || nnodes == 0 || (!tri_ids && nids)) return fail(c, RT_E_INVALID, "rt_upload_bvh: null array");
+    for (uint32_t k = 0; k < nids; k++)
+        if (tri_ids[k] >= c->ntris) return fail(c, RT_E_INVALID, "rt_upload_bvh: triangle id out of range");
+    // validate nodes reachable from the root (bvh.wgsl:168-179 walk)
+    std::vector<uint8_t> seen(nnodes, 0);
+    std::vector<uint32_t> stack{0};
+    while (!stack.empty()) {
+        const uint32_t i = stack.back();
+        stack.pop_back();
+        if (seen[i]) continue;
+        seen[i] = 1;
+        const rt_gpu_node& n = nodes[i];
+        if (n.n_prims > 0) {
+            if ((uint64_t)n.offset_ptr + n.n_prims > nids) return fail(c, RT_E_INVALID, "rt_upload_bvh: leaf range");
+        } else {
+            if ((uint64_t)i + 1 >= nnodes || n.offset_ptr >= nnodes)
+                return fail(c, RT_E_INVALID, "rt_upload_bvh: child index out of range");
+            stack.push_back(i + 1);
+            stack.push_back(n.offset_ptr);
+        }
+    }
+    std::vector<float> recs;
+    build_recs(c->h_pos, c->h_idx, tri_ids, nids, recs);
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_bvh = false;
+    int r;
+    if ((r = upload(c, c->bvh_nodes, nodes, (size_t)nnodes * sizeof(rt_gpu_node)))) return r;
+    if ((r = upload(c, c->bvh_recs, recs.data(), recs.size() * 4))) return r;
+    if ((r = upload(c, c->bvh_ids, tri_ids, (size_t)nids * 4))) return r;
+    c->bvh_nnodes = nnodes;
+    c->has_bvh = true;
+    return RT_OK;
+}
+
+int rt_set_uniforms(rt_ctx* c, const rt_uniform* u, const float* jitter)
+{
+    if (!c || !u) return RT_E_INVALID;
+    if (u->resolution[0] == 0 || u->resolution[1] == 0) return fail(c, RT_E_INVALID, "rt_set_uniforms: zero resolution");
+    if (u->subdivision_level == 0 || u->subdivision_level > 10)
+        return fail(c, RT_E_INVALID, "rt_set_uniforms: subdivision_level must be in [1,10] (uniform.rs:36)");
+    if (!jitter && u->subdivision_level != 1)
+        return fail(c, RT_E_INVALID, "rt_set_uniforms: jitter table required when subdivision_level > 1");
+    if (int r = set_dev(c)) return r;
+    c->u = *u;
+    c->has_u = true;
+    c->has_jitter = false;
+    if (jitter) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        const size_t bytes = (size_t)u->subdivision_level * u->subdivision_level * 2 * sizeof(float);
+        if (int r = upload(c, c->jitter, jitter, bytes)) return r;
+        c->has_jitter = true;
+    }
+    return RT_OK;
+}
+
+int rt_set_environment(rt_ctx* c, const float rgb[3])
+{
+    if (!c || !rgb) return RT_E_INVALID;
+    memcpy(c->env, rgb, sizeof c->env);
+    return RT_OK;
+}
+
+static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
+{
+    if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
+    if (mode < RT_MODE_W1E6 || mode > RT_MODE_W9E1) return fail(c, RT_E_INVALID, "rt_render: bad mode");
+    if (mode == RT_MODE_W1E6) {
+        if (trav != RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "W1E6 is analytic: traverse must be NONE");
+    } else {
+        if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_render: no mesh uploaded");
+        if (trav == RT_TRAVERSE_BSP && !c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_render: no BSP uploaded");
+        if (trav == RT_TRAVERSE_BVH && !c->has_bvh) return fail(c, RT_E_NOT_READY, "rt_render: no BVH uploaded");
+        if (trav == RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "mesh modes need BSP or BVH");
+        if (mode == RT_MODE_W7E3 && c->nlights < 2)
+            return fail(c, RT_E_INVALID, "W7E3 samples area lights: the mesh has no emissive (illum 1) triangle");
+        if ((mode == RT_MODE_W6E1 || mode == RT_MODE_PROJECT) && trav == RT_TRAVERSE_BSP && !c->has_bsp)
+            return fail(c, RT_E_NOT_READY, "rt_render: W6E1/PROJECT need the BSP root AABB");
+    }
+    if (!L.accum) return fail(c, RT_E_INVALID, "rt_render: accum buffer required");
+    if (int r = set_dev(c)) return r;
+    rtk::DevScene S;
+    memset(&S, 0, sizeof S);
+    S.pos = c->pos.as<float4>();
+    S.nrm = c->nrm.as<float4>();
+    S.tri_idx = c->idx.as<uint4>();
+    S.mats = c->mats.as<rt_material>();
+    S.lights = c->lights.as<uint32_t>();
+    S.nverts = c->nverts;
+    S.ntris = c->ntris;
+    S.nmats = c->nmats;
+    S.nlights = c->nlights;
+    S.bsp_nodes = c->bsp_nodes.as<uint2>();
+    S.bsp_recs = c->bsp_recs.as<float4>();
+    S.bsp_ids = c->bsp_ids.as<uint32_t>();
+    S.bsp_depth = c->bsp_depth;
+    memcpy(S.aabb, c->aabb, sizeof S.aabb);
+    S.bvh_nodes = c->bvh_nodes.as<float4>();
+    S.bvh_recs = c->bvh_recs.as<float4>();
+    S.bvh_ids = c->bvh_ids.as<uint32_t>();
+    S.bvh_nnodes = c->bvh_nnodes;
+    L.u = c->u;
+    L.jitter = c->has_jitter ? c->jitter.as<float>() : nullptr;
+    memcpy(L.env, c->env, sizeof L.env);
+    L.work_counter = c->work.as<uint32_t>();
+    L.counters = c->counters.as<unsigned long long>();
+    HIPCHK(c, hipMemsetAsync(c->work.p, 0, 64, c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 16 * sizeof(unsigned long long), c->stream));
+    if (L.nwork == 0) return RT_OK;
+    int r = rtk::launch_render(S, L, mode, trav, c->detail, c->num_cus, c->waves_per_cu, c->stream);
+    if (r) return fail(c, r, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (counts) return rt_last_counts(c, counts);
+    return RT_OK;
+}
+
+int rt_render(rt_ctx* c, rt_mode mode, rt_traverse trav, const rt_tile* region, uint32_t first_iter, uint32_t spp,
+              float* accum, uint32_t* ids, rt_ray_counts* counts)
+{
+    if (!c || !region) return RT_E_INVALID;
+    if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
+    const uint32_t W = c->u.resolution[0], H = c->u.resolution[1];
+    if ((uint64_t)region->x0 + region->w > W || (uint64_t)region->y0 + region->h > H)
+        return fail(c, RT_E_INVALID, "rt_render: region outside uniforms.resolution");
+    rtk::DevLaunch L;
+    memset(&L, 0, sizeof L);
+    L.tileset = 0;
+    L.x0 = region->x0;
+    L.y0 = region->y0;
+    L.w = region->w;
+    L.h = region->h;
+    L.rank = 0;
+    L.nranks = 1;
+    L.tiles_x = (region->w + 7) / 8;
+    L.tiles_y = (region->h + 7) / 8;
+    L.nwork = L.tiles_x * L.tiles_y;
+    L.first_iter = first_iter;
+    L.spp = spp;
+    L.accum = reinterpret_cast<float4*>(accum);
+    L.ids = ids;
+    return render_common(c, mode, trav, L, counts);
+}
+
+uint32_t rt_tileset_local_tiles(uint32_t width, uint32_t height, uint32_t nranks)
+{
+    if (nranks == 0) return 0;
+    const uint64_t t = (uint64_t)((width + 7) / 8) * ((height + 7) / 8);
+    return (uint32_t)((t + nranks - 1) / nranks);
+}
+
+int rt_render_tiles(rt_ctx* c, rt_mode mode, rt_traverse trav, const rt_tileset* ts, uint32_t first_iter,
+                    uint32_t spp, float* accum, uint32_t* ids, rt_ray_counts* counts)
+{
+    if (!c || !ts) return RT_E_INVALID;
+    if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render_tiles: uniforms not set");
+    if (ts->nranks == 0 || ts->rank >= ts->nranks) return fail(c, RT_E_INVALID, "rt_render_tiles: bad rank/nranks");
+    const uint32_t W = c->u.resolution[0], H = c->u.resolution[1];
+    rtk::DevLaunch L;
+    memset(&L, 0, sizeof L);
+    L.tileset = 1;
+    L.x0 = 0;
+    L.y0 = 0;
+    L.w = W;
+    L.h = H;
+    L.rank = ts->rank;
+    L.nranks = ts->nranks;
+    L.tiles_x = (W + 7) / 8;
+    L.tiles_y = (H + 7) / 8;
+    L.nwork = rt_tileset_local_tiles(W, H, ts->nranks);
+    L.first_iter = first_iter;
+    L.spp = spp;
+    L.accum = reinterpret_cast<float4*>(accum);
+    L.ids = ids;
+    return render_common(c, mode, trav, L, counts);
+}
+
+int rt_unpack_tiles(rt_ctx* c, uint32_t width, uint32_t height, uint32_t nranks, const float* packed_accum,
+                    const uint32_t* packed_ids, float* frame_accum, uint32_t* frame_ids)
+{
+    if (!c || nranks == 0) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    const uint32_t lt = rt_tileset_local_tiles(width, height, nranks);
+    int r = rtk::launch_unpack(width, height, nranks, lt, reinterpret_cast<const float4*>(packed_accum), packed_ids,
+                               reinterpret_cast<float4*>(frame_accum), frame_ids, c->stream);
+    if (r) return fail(c, r, "rt_unpack_tiles: launch failed");
+    return RT_OK;
+}
+
+int rt_last_counts(rt_ctx* c, rt_ray_counts* counts)
+{
+    if (!c || !counts) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    unsigned long long h[16];
+    HIPCHK(c, hipMemcpyAsync(h, c->counters.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint64_t* dst = reinterpret_cast<uint64_t*>(counts);
+    for (size_t i = 0; i < sizeof(rt_ray_counts) / sizeof(uint64_t); i++) dst[i] = h[i];
+    c->last = *counts;
+    return RT_OK;
+}
+
+int rt_selftest_math(rt_ctx* c, uint32_t n, float lo, float hi, uint32_t* mismatches)
+{
+    if (!c || !mismatches || n == 0) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    std::vector<float> in(n), hout((size_t)n * rtk::kMathOuts), dout((size_t)n * rtk::kMathOuts);
+    uint32_t s = 12345u;
+    for (uint32_t i = 0; i < n; i++) {
+        s = s * 1664525u + 1013904223u;
+        const float t = (float)i / (float)n;
+        in[i] = lo + (hi - lo) * t + ((float)(s >> 8) * (1.0f / 16777216.0f) - 0.5f) * ((hi - lo) / (float)n);
+    }
+    rtk::host_math(in.data(), hout.data(), n);
+    DevBuf din, dres;
+    if (int r = upload(c, din, in.data(), in.size() * 4)) return r;
+    HIPCHK(c, dres.alloc(dout.size() * 4));
+    if (rtk::launch_selftest_math(din.as<float>(), dres.as<float>(), n, c->stream))
+        return fail(c, RT_E_DEVICE, "rt_selftest_math: launch failed");
+    HIPCHK(c, hipMemcpyAsync(dout.data(), dres.p, dout.size() * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    uint32_t bad = 0;
+    for (size_t i = 0; i < dout.size(); i++) {
+        uint32_t a, b;
+        memcpy(&a, &hout[i], 4);
+        memcpy(&b, &dout[i], 4);
+        const bool both_nan = std::isnan(hout[i]) && std::isnan(dout[i]);
+        if (a != b && !both_nan) bad++;
+    }
+    *mismatches = bad;
+    return RT_OK;
+}
+
+int rt_upload_mesh_host(rt_ctx* c, const rt_mesh_host* m)
+{
+    if (!c || !m) return RT_E_INVALID;
+    return rt_upload_mesh(c, m->pos.data(), m->nrm.data(), m->nverts(), m->idx.data(), m->ntris(), m->mats.data(),
+                          (uint32_t)m->mats.size(), m->lights.data(), (uint32_t)m->lights.size());
+}
+
+int rt_upload_bsp_host(rt_ctx* c, const rt_bsp_host* b)
+{
+    if (!c || !b) return RT_E_INVALID;
+    return rt_upload_bsp(c, b->aabb, b->tree.data(), b->planes.data(), (uint32_t)b->planes.size(), b->ids.data(),
+                         (uint32_t)b->ids.size(), b->max_depth);
+}
+
+int rt_upload_bvh_host(rt_ctx* c, const rt_bvh_host* b)
+{
+    if (!c || !b) return RT_E_INVALID;
+    return rt_upload_bvh(c, b->nodes.data(), (uint32_t)b->nodes.size(), b->tri_ids.data(), (uint32_t)b->tri_ids.size());
+}
+
+}  // extern "C"

@@ -1,0 +1,68 @@
+// rt_internal.h -- launch interface between the C ABI layer (rt_api.cpp) and
+// the gfx950 kernels (rt_kernels.hip).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/rt.h"
+
+namespace rtk {
+
+// Device-resident scene, in the layout the kernels read (DESIGN.md "Data layout in HBM").
+struct DevScene {
+    // mesh (src/bindings/storage_mesh.rs): positions/normals float4, index uint4 (v0,v1,v2,mat)
+    const float4* pos;
+    const float4* nrm;
+    const uint4* tri_idx;
+    const rt_material* mats;
+    const uint32_t* lights;
+    uint32_t nverts, ntris, nmats, nlights;
+    // BSP: 8-byte nodes {x = axis|count<<2, y = plane bits (interior) / first id (leaf)};
+    // children implicit (2i+1, 2i+2, src/data_structures/bsp_tree.rs:137-140).
+    const uint2* bsp_nodes;
+    const float4* bsp_recs;       // 3 x float4 per treeIds slot: v0, e0=v1-v0, e1=v2-v0, n=cross(e0,e1)
+    const uint32_t* bsp_ids;      // treeIds
+    uint32_t bsp_depth;           // MAX_LEVEL
+    float aabb[6];                // root BboxGpu min.xyz, max.xyz
+    // BVH: GpuNode as 2 x float4; records in bvh_triangles order
+    const float4* bvh_nodes;
+    const float4* bvh_recs;
+    const uint32_t* bvh_ids;
+    uint32_t bvh_nnodes;
+};
+
+// Work mapping + outputs of one launch.
+struct DevLaunch {
+    rt_uniform u;
+    const float* jitter;          // subdiv^2 float2 (device), may be null when subdiv == 1
+    float env[3];
+    // region mode (tileset == 0): 8x8 tiles over [x0,x0+w) x [y0,y0+h), row-major region output
+    // tileset mode (tileset == 1): global 8x8 tiles t = l*nranks + rank, packed output
+    uint32_t tileset;
+    uint32_t x0, y0, w, h;
+    uint32_t rank, nranks;
+    uint32_t tiles_x, tiles_y;    // tile grid (of the region, or of the frame)
+    uint32_t nwork;               // work items (tiles) in this launch
+    uint32_t first_iter, spp;
+    float4* accum;
+    uint32_t* ids;
+    uint32_t* work_counter;       // zeroed before launch
+    unsigned long long* counters; // 10 x u64, zeroed before launch (rt_ray_counts order)
+};
+
+// Launch the kernel for (mode, trav); detail = counting instantiation.
+int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traverse trav, bool detail,
+                  int num_cus, int waves_per_cu, hipStream_t stream);
+
+int launch_unpack(uint32_t width, uint32_t height, uint32_t nranks, uint32_t local_tiles,
+                  const float4* packed_accum, const uint32_t* packed_ids, float4* frame_accum,
+                  uint32_t* frame_ids, hipStream_t stream);
+
+int launch_selftest_math(const float* in, float* out, uint32_t n, hipStream_t stream);
+
+// Host reference of the pinned math for the self test (same header, host compile).
+void host_math(const float* in, float* out, uint32_t n);
+
+constexpr int kMathOuts = 8;   // outputs per input in the math self test
+
+}  // namespace rtk

@@ -1,0 +1,108 @@
+"""Headless RenderState: mirror of src/render_state.rs (setup_rendering
+:161-265, update :467-481, render :483-561) and of the progressive loop of
+src/lib.rs:321-363, on top of the C ABI.
+
+Differences from the windowed reference, all deliberate:
+  * no window/surface: aspect = W/H of SceneDescriptor.res (the reference
+    uses the window's inner size, render_state.rs:563-566);
+  * the accumulation "texture" is an HBM float4 array (linear RGBA32F), and
+    the display transform pow(., 1.5) is left to the caller;
+  * the W9E1 equirectangular hdri0 is a constant environment colour
+    (rt_set_environment) -- texture sampling is out of scope;
+  * a missing bunny.obj can be replaced by the deterministic stand-in
+    (bunny_standin=True), since the reference checkout lacks it.
+"""
+import os
+
+import numpy as np
+
+from . import _ffi as F
+from .core import BspTree, Bvh, Context, Mesh, make_uniform
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ASSETS = os.path.join(REPO, "assets", "models")
+
+
+class RenderState:
+    def __init__(self, scene, device=0, ctx=None, models_dir=ASSETS, bunny_standin=True, selection1=0,
+                 env=(1.0, 1.0, 1.0), resolution=None):
+        self.ctx = ctx if ctx is not None else Context(device)
+        self.models_dir = models_dir
+        self.bunny_standin = bunny_standin
+        self.selection1 = selection1
+        self.env = env
+        self.resolution = resolution
+        self.progressive = True
+        self.iteration = 0
+        self.setup_rendering(scene)
+
+    # render_state.rs:161-265
+    def setup_rendering(self, scene):
+        if scene.mode is None:
+            raise F.RtError(F.RT_E_UNSUPPORTED, f"{scene.shader} is outside the hot path (SURVEY.md section 2)")
+        self.scene = scene
+        self.mode = scene.mode
+        self.width, self.height = self.resolution or scene.res
+        self.mesh = self.bsp = self.bvh = None
+        if scene.mode == "W1E6":
+            self.trav = "NONE"
+        else:
+            self.trav = scene.traverse_type
+            self.mesh = self._load_model(scene.model)
+            self.ctx.upload_mesh(self.mesh)
+            if self.trav == "BSP":
+                self.bsp = self.mesh.bsp_tree()   # Mesh::bsp_tree, mesh.rs:229-231 (depth 20, leaf 4)
+                self.ctx.upload_bsp(self.bsp)
+            else:
+                self.bvh = self.mesh.bvh()        # Mesh::bvh, mesh.rs:233-239 (leaf 4)
+                self.ctx.upload_bvh(self.bvh)
+        self.ctx.set_environment(self.env)
+        npx = self.width * self.height
+        self.accum = self.ctx.alloc(npx * 16)
+        self.accum.zero()
+        self.ids = self.ctx.alloc(npx * 4)
+        self.iteration = 0
+        self.update()
+
+    def _load_model(self, model):
+        path = os.path.join(self.models_dir, model)
+        if not os.path.exists(path) and model == "bunny.obj" and self.bunny_standin:
+            return Mesh.synth_bunny()
+        return Mesh.from_obj(path)
+
+    def load_scene(self, scene):
+        """RenderState::load_scene (render_state.rs:314-334): full rebuild."""
+        self.setup_rendering(scene)
+
+    # render_state.rs:467-481
+    def update(self):
+        cam = self.scene.camera
+        self.uniform = make_uniform(cam.eye, cam.target, cam.up, cam.constant, self.width, self.height,
+                                    selection1=self.selection1, iteration=self.iteration)
+        self.ctx.set_uniforms(self.uniform)
+
+    # render_state.rs:483-561 (+ lib.rs:349-354 iteration advance)
+    def render(self, spp=1, counts=False):
+        first = self.iteration if self.progressive else 0
+        c = self.ctx.render(self.mode, self.trav, (0, 0, self.width, self.height), first, spp, self.accum.ptr,
+                            self.ids.ptr, counts=counts)
+        if self.progressive and self.mode in ("W7E3", "W9E1"):
+            self.iteration += spp
+        self.update()
+        return c
+
+    def reset_iteration(self):
+        self.iteration = 0
+        self.update()
+
+    def frame(self):
+        """Linear accumulation [H, W, 4] float32 (the RenderDestination texture)."""
+        return self.accum.to_numpy(np.float32, (self.height, self.width, 4))
+
+    def hit_ids(self):
+        return self.ids.to_numpy(np.uint32, (self.height, self.width))
+
+    @staticmethod
+    def display(accum):
+        """fs_main's frame output: saturate(pow(accum, 1.5)) (w7e3.wgsl:265)."""
+        return np.clip(np.power(np.maximum(accum[..., :3], 0), 1.5), 0, 1)

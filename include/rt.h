@@ -1,0 +1,329 @@
+/*
+ * rt.h -- C ABI of the MI355X-native hot path of cakarsubasi/02562_raytracer.
+ *
+ * The reference renders one frame per `RenderState::render()` call
+ * (src/render_state.rs:483-561): a full-screen quad whose fragment shader
+ * (`fs_main` of res/shaders/{w6e1,project,w7e3,w9e1,w1e6}.wgsl) traces one path
+ * per pixel through the BSP (res/shaders/bsp.wgsl:10-81) or HLBVH
+ * (res/shaders/bvh.wgsl:154-191).  This library replaces, behind plain C
+ * pointers and sizes:
+ *   - the wgpu device/queue wrapper          src/gpu_handles.rs:9-14, 72-92
+ *   - the storage-buffer uploads             src/bindings/{storage_mesh,bsp_tree,bvh,uniform}.rs
+ *   - the render pass + accumulation copy    src/render_state.rs:483-561
+ *   - the fragment shader itself             res/shaders/<scene>.wgsl (HIP kernels for gfx950)
+ * and exposes the host-side builders that feed it (the reference computes these
+ * in Rust before upload):
+ *   - Mesh::from_obj / Mesh::load            src/mesh.rs:78-202
+ *   - BspTree::new + bsp_array + primitive_ids  src/data_structures/bsp_tree.rs:45,120,79
+ *   - hlbvh::Bvh::new + flatten + triangles  src/data_structures/hlbvh.rs:36,195,237
+ *
+ * Conventions:
+ *   - every function returns RT_OK (0) or a negative RT_E_* code; no exceptions
+ *     cross the ABI; rt_last_error() gives a message for the last failure;
+ *   - uploads copy from caller-owned host arrays (as wgpu create_buffer_init);
+ *     the context owns all device memory it allocates;
+ *   - a context is bound to one HIP device and is not thread-safe: use one
+ *     context per GPU and per host thread (the reference uses its RenderState
+ *     from the single "Render Thread", src/lib.rs:305-307);
+ *   - output buffers passed to rt_render* are DEVICE pointers (HBM resident);
+ *     their layout is documented per function.
+ */
+#ifndef RT02562_RT_H
+#define RT02562_RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define RT_OK            0
+#define RT_E_INVALID    (-1)  /* bad argument / malformed structure          */
+#define RT_E_OOM        (-2)  /* device allocation failed (SurfaceError::OutOfMemory, src/lib.rs:345) */
+#define RT_E_DEVICE     (-3)  /* HIP runtime error                           */
+#define RT_E_NOT_READY  (-4)  /* render called before the needed upload      */
+#define RT_E_IO         (-5)  /* file could not be read / parsed             */
+#define RT_E_UNSUPPORTED (-6) /* mode/traversal combination not implemented  */
+
+/* ---- plain data types (byte-compatible with the reference GPU structs) -- */
+
+/* Material, 64 B: src/mesh.rs:12-20 (WGSL struct src/bindings/storage_mesh.rs:392-397) */
+typedef struct rt_material {
+    float diffuse[4];
+    float ambient[4];
+    float specular[4];
+    uint32_t emissive;      /* MTL illum; == 1 marks an area light (storage_mesh.rs:322) */
+    uint32_t _pad[3];
+} rt_material;
+
+/* HLBVH GpuNode, 32 B: src/data_structures/hlbvh.rs:508-515 */
+typedef struct rt_gpu_node {
+    float min[3];
+    uint32_t offset_ptr;    /* leaf: first index into tri_ids; interior: right child */
+    float max[3];
+    uint32_t n_prims;       /* 0 = interior (left child is node+1) */
+} rt_gpu_node;
+
+/* Uniform block, 80 B: src/bindings/uniform.rs:6-34 */
+typedef struct rt_uniform {
+    float camera_pos[3];
+    float camera_constant;
+    float camera_look_at[3];
+    float aspect_ratio;
+    float camera_up[3];
+    uint32_t selection1;     /* shader selector (0 = Lambertian) */
+    uint32_t selection2;
+    uint32_t subdivision_level;
+    uint32_t use_texture;
+    uint32_t iteration;      /* progressive frame index (overridden by first_iter) */
+    float uv_scale[2];
+    uint32_t resolution[2];  /* full-frame W, H (global pixel space) */
+} rt_uniform;
+
+/* Which scene shader the kernel restates (SceneDescriptor.shader, src/scenes.rs:19-29). */
+typedef enum rt_mode {
+    RT_MODE_W1E6    = 0,  /* res/shaders/w1e6.wgsl: analytic sphere/plane/triangle, no mesh  */
+    RT_MODE_W6E1    = 1,  /* res/shaders/w6e1.wgsl: primary rays, directional light, split vertex layout */
+    RT_MODE_PROJECT = 2,  /* res/shaders/project.wgsl: as W6E1, combined layout, ambient*0.1 */
+    RT_MODE_W7E3    = 3,  /* res/shaders/w7e3.wgsl: area-light path tracer, progressive       */
+    RT_MODE_W9E1    = 4   /* res/shaders/w9e1.wgsl: dummy-light path tracer, environment escape */
+} rt_mode;
+
+/* SceneDescriptor.traverse_type, src/scenes.rs:13-17 */
+typedef enum rt_traverse {
+    RT_TRAVERSE_BSP  = 0,
+    RT_TRAVERSE_BVH  = 1,
+    RT_TRAVERSE_NONE = 2   /* only valid with RT_MODE_W1E6 */
+} rt_traverse;
+
+/* A rectangle of the frame in GLOBAL pixel coordinates. */
+typedef struct rt_tile {
+    uint32_t x0, y0, w, h;
+} rt_tile;
+
+/* Interleaved 8x8-tile partition of the full frame for multi-GPU rendering
+ * (SURVEY.md 8(e)): tile t (row-major over ceil(W/8) x ceil(H/8) tiles) is owned
+ * by rank t % nranks.  Global pixel coordinates keep PRNG seeds, and therefore
+ * images, identical for every nranks. */
+typedef struct rt_tileset {
+    uint32_t rank;
+    uint32_t nranks;
+} rt_tileset;
+
+#define RT_TILE_DIM 8u    /* tile edge in pixels: one wave64 = one 8x8 tile */
+
+/* Per-launch counters.  primary/shadow/bounce are always filled; the traversal
+ * detail counters are filled only when RT_OPT_DETAIL_COUNTERS is enabled (a
+ * separate, slower kernel instantiation used to price algorithmic bytes). */
+typedef struct rt_ray_counts {
+    uint64_t samples;        /* pixel-samples traced                       */
+    uint64_t primary;        /* camera rays                                */
+    uint64_t shadow;         /* shadow (visibility) rays                   */
+    uint64_t bounce;         /* indirect closest-hit rays                  */
+    uint64_t node_interior;  /* BSP interior node visits                   */
+    uint64_t node_leaf;      /* BSP leaf visits                            */
+    uint64_t bvh_pops;       /* BVH node pops                              */
+    uint64_t ids_read;       /* treeIds / bvh_triangles reads              */
+    uint64_t tri_tests;      /* ray-triangle tests                         */
+    uint64_t tri_accepts;    /* accepted (closer) hits                     */
+} rt_ray_counts;
+
+/* ---- options (rt_set_option) ------------------------------------------- */
+#define RT_OPT_DETAIL_COUNTERS 1  /* 0/1: use the counting kernel instantiation    */
+#define RT_OPT_WAVES_PER_CU    2  /* persistent grid size: waves per CU (default 16) */
+
+/* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
+
+typedef struct rt_ctx rt_ctx;   /* one HIP device + stream + the device-resident scene */
+
+/* Number of HIP devices (~ gpu_handles::self_test, src/gpu_handles.rs:72-92). */
+int rt_device_count(int* count);
+
+/* Create a context on HIP device `device` (~ GPUHandles::new / RenderState::new
+ * device part, src/render_state.rs:66-106).  Creates its own non-blocking stream. */
+int rt_create(int device, rt_ctx** out);
+void rt_destroy(rt_ctx* ctx);
+
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream)
+ * instead of the context's own stream; NULL restores the own stream. */
+int rt_set_stream(rt_ctx* ctx, void* hip_stream);
+void* rt_get_stream(rt_ctx* ctx);
+int rt_synchronize(rt_ctx* ctx);
+
+int rt_set_option(rt_ctx* ctx, int option, int64_t value);
+
+/* Message describing the last failure on this context (or the last
+ * context-less failure when ctx == NULL).  Never NULL. */
+const char* rt_last_error(const rt_ctx* ctx);
+
+/* Device memory for frame buffers (the RenderSource/RenderDestination
+ * textures of src/bindings/texture.rs:285-407 become plain HBM arrays).
+ * Copies synchronize the context stream; memset is asynchronous on it. */
+int rt_device_alloc(rt_ctx* ctx, size_t bytes, void** dptr);
+int rt_device_free(rt_ctx* ctx, void* dptr);
+int rt_memcpy_to_host(rt_ctx* ctx, void* dst, const void* src_dev, size_t bytes);
+int rt_memcpy_to_device(rt_ctx* ctx, void* dst_dev, const void* src, size_t bytes);
+int rt_memset_device(rt_ctx* ctx, void* dst_dev, int value, size_t bytes);
+
+/* HIP-event timer on the context stream (RenderStats, src/tools.rs:4-61,
+ * times render() on the host; this times the device work). */
+int rt_timer_start(rt_ctx* ctx);
+int rt_timer_stop(rt_ctx* ctx, float* ms);   /* synchronizes */
+
+/* ---- uploads (replace the src/bindings/ create_buffer_init calls) ------------- */
+
+/* Mesh + materials + light list (src/bindings/storage_mesh.rs:13-26, 82-110,
+ * 201-236, 297-332).  pos_vec4 / nrm_vec4: nverts x float4 (w ignored);
+ * nrm_vec4 may be NULL (zero normals, as mesh.rs:165-171).  idx_vec4u: ntris x
+ * (v0, v1, v2, material).  light_idx[0] must be the UINT32_MAX sentinel
+ * (storage_mesh.rs:325-326); light_idx may be NULL to derive the list from
+ * materials[].emissive == 1. */
+int rt_upload_mesh(rt_ctx* ctx,
+                   const float* pos_vec4, const float* nrm_vec4, uint32_t nverts,
+                   const uint32_t* idx_vec4u, uint32_t ntris,
+                   const rt_material* mats, uint32_t nmats,
+                   const uint32_t* light_idx, uint32_t nlight);
+
+/* Flattened BSP (src/bindings/bsp_tree.rs:167-203): aabb = BboxGpu (min.xyz,
+ * pad, max.xyz, pad); tree_vec4u = nnodes x (axis|count<<2, first_id, left,
+ * right) with nnodes == 2^(max_depth+1)-1; planes = nnodes floats; ids = nids
+ * triangle indices.  Requires a prior rt_upload_mesh (triangles are repacked
+ * in treeIds order on upload). */
+int rt_upload_bsp(rt_ctx* ctx, const float aabb[8],
+                  const uint32_t* tree_vec4u, const float* planes, uint32_t nnodes,
+                  const uint32_t* ids, uint32_t nids, uint32_t max_depth);
+
+/* Flattened HLBVH (src/bindings/bvh.rs:75-93). Requires a prior rt_upload_mesh. */
+int rt_upload_bvh(rt_ctx* ctx, const rt_gpu_node* nodes, uint32_t nnodes,
+                  const uint32_t* tri_ids, uint32_t nids);
+
+/* Uniforms + jitter table (src/bindings/uniform.rs:163-176).  jitter holds
+ * subdivision_level^2 float2 offsets (may be NULL when subdivision_level == 1:
+ * compute_jitters returns (0,0), uniform.rs:261-263). */
+int rt_set_uniforms(rt_ctx* ctx, const rt_uniform* u, const float* jitter);
+
+/* Environment radiance returned on escape by RT_MODE_W9E1 (stands in for the
+ * equirectangular hdri0 texture, res/shaders/w9e1.wgsl:232-241). Default (1,1,1). */
+int rt_set_environment(rt_ctx* ctx, const float rgb[3]);
+
+/* ---- render (replaces RenderState::render, src/render_state.rs:483-561) -- */
+
+/* Trace `spp` progressive iterations first_iter .. first_iter+spp-1 for every
+ * pixel of `region` (global pixel coordinates inside uniforms.resolution).
+ *   accum_rgba32f: DEVICE, region.w*region.h float4, row-major over the region,
+ *     in/out: holds the accumulation of iterations < first_iter (read when
+ *     first_iter > 0; the RenderDestination texture, render_state.rs:541-555),
+ *     and receives max(vec4(accum,1),0) (w7e3.wgsl:261-271).  For W1E6/W6E1/
+ *     PROJECT it receives the linear per-frame result (before pow(.,1.5)).
+ *   primary_hit_ids: DEVICE or NULL, region.w*region.h u32: triangle index of
+ *     the primary hit of the LAST traced iteration, UINT32_MAX on miss.
+ *   counts: host pointer or NULL; when non-NULL the call synchronizes and
+ *     stores this launch's counters. */
+int rt_render(rt_ctx* ctx, rt_mode mode, rt_traverse trav, const rt_tile* region,
+              uint32_t first_iter, uint32_t spp,
+              float* accum_rgba32f, uint32_t* primary_hit_ids,
+              rt_ray_counts* counts);
+
+/* Same, over the 8x8 tiles owned by `ts` (multi-GPU framebuffer tiling).
+ * Outputs are PACKED: local tile l (the l-th tile with t % nranks == rank,
+ * i.e. global tile t = l*nranks + rank) occupies pixels [l*64, l*64+64),
+ * row-major inside the tile.  Buffers hold rt_tileset_local_tiles() * 64 px. */
+int rt_render_tiles(rt_ctx* ctx, rt_mode mode, rt_traverse trav, const rt_tileset* ts,
+                    uint32_t first_iter, uint32_t spp,
+                    float* accum_rgba32f, uint32_t* primary_hit_ids,
+                    rt_ray_counts* counts);
+
+/* Number of local tiles rank `rank` owns for a W x H frame (equal for all ranks
+ * rounded up, so packed buffers have one size: ceil(ntiles / nranks)). */
+uint32_t rt_tileset_local_tiles(uint32_t width, uint32_t height, uint32_t nranks);
+
+/* Scatter gathered packed buffers (nranks x local_tiles x 64 px, rank-major as
+ * produced by an all-gather) into a row-major W x H frame, on the context's
+ * stream.  Either pair of pointers may be NULL. */
+int rt_unpack_tiles(rt_ctx* ctx, uint32_t width, uint32_t height, uint32_t nranks,
+                    const float* packed_accum, const uint32_t* packed_ids,
+                    float* frame_accum, uint32_t* frame_ids);
+
+/* Counters of the most recent launch (synchronizes). */
+int rt_last_counts(rt_ctx* ctx, rt_ray_counts* counts);
+
+/* Device-vs-host self check of the pinned f32 math (sqrt, division, the
+ * rt_detmath.h transcendentals) over n inputs in [lo, hi]; returns the number
+ * of bit mismatches in *mismatches. */
+int rt_selftest_math(rt_ctx* ctx, uint32_t n, float lo, float hi, uint32_t* mismatches);
+
+/* ---- host-side builders (the Rust code above the reference's GPU boundary) */
+
+typedef struct rt_mesh_host rt_mesh_host;   /* owns Mesh arrays (src/mesh.rs:35-41) */
+typedef struct rt_mesh_view {
+    const float* vertices;     /* nverts x float4 */
+    const float* normals;      /* nverts x float4 */
+    const uint32_t* indices;   /* ntris x (v0,v1,v2,material) */
+    const rt_material* materials;
+    const uint32_t* lights;    /* nlights entries, [0] = UINT32_MAX sentinel */
+    uint32_t nverts, ntris, nmats, nlights;
+} rt_mesh_view;
+
+/* Mesh::from_obj with tobj 4.0 semantics (single_index, fan triangulation,
+ * per-group models, MTL Kd/Ka/Ks/illum), src/mesh.rs:78-202. */
+int rt_mesh_load_obj(const char* path, rt_mesh_host** out);
+/* Wrap caller arrays into a host mesh (copies). normals/materials may be NULL. */
+int rt_mesh_from_arrays(const float* pos_vec4, const float* nrm_vec4, uint32_t nverts,
+                        const uint32_t* idx_vec4u, uint32_t ntris,
+                        const rt_material* mats, uint32_t nmats, rt_mesh_host** out);
+/* Deterministic synthetic meshes for the configs the reference cannot supply:
+ *   kind 0: displaced-sphere "bunny" stand-in (~ntris triangles, bunny bbox);
+ *   kind 1: 10M-style random triangle soup, centres U[-1,1]^3, half-size 0.01;
+ *   kind 2: nx x nz grid of copies of `src` translated by `spacing` (instancing
+ *           flattened into one mesh; the reference has no instancing). */
+int rt_mesh_synth_bunny(uint32_t ntris_target, uint32_t seed, rt_mesh_host** out);
+int rt_mesh_synth_soup(uint32_t ntris, uint32_t seed, rt_mesh_host** out);
+int rt_mesh_synth_grid(const rt_mesh_host* src, uint32_t nx, uint32_t nz, float spacing,
+                       rt_mesh_host** out);
+int rt_mesh_scale(rt_mesh_host* m, float factor);   /* Mesh::scale, src/mesh.rs:246-252 */
+int rt_mesh_view_get(const rt_mesh_host* m, rt_mesh_view* view);
+void rt_mesh_free(rt_mesh_host* m);
+
+typedef struct rt_bsp_host rt_bsp_host;
+typedef struct rt_bsp_view {
+    const uint32_t* tree;     /* nnodes x vec4u */
+    const float* planes;      /* nnodes */
+    const uint32_t* ids;      /* nids */
+    float aabb[8];            /* BboxGpu */
+    uint32_t nnodes, nids, max_depth;
+} rt_bsp_view;
+
+/* BspTree::new(bboxes, max_depth, max_leaf) + bsp_array() + primitive_ids(),
+ * bit-identical to the reference's f32 arithmetic; nthreads <= 0 = hardware. */
+int rt_bsp_build(const rt_mesh_host* mesh, uint32_t max_depth, uint32_t max_leaf,
+                 int nthreads, rt_bsp_host** out);
+int rt_bsp_view_get(const rt_bsp_host* b, rt_bsp_view* view);
+void rt_bsp_free(rt_bsp_host* b);
+
+typedef struct rt_bvh_host rt_bvh_host;
+typedef struct rt_bvh_view {
+    const rt_gpu_node* nodes;
+    const uint32_t* tri_ids;
+    uint32_t nnodes, nids;
+} rt_bvh_view;
+
+/* hlbvh::Bvh::new(mesh, max_prims) + flatten() + triangles(). Equal Morton
+ * codes are ordered by primitive index (the reference's rdst order is
+ * implementation-defined). */
+int rt_bvh_build(const rt_mesh_host* mesh, uint32_t max_prims, rt_bvh_host** out);
+int rt_bvh_view_get(const rt_bvh_host* b, rt_bvh_view* view);
+void rt_bvh_free(rt_bvh_host* b);
+
+/* Convenience: upload a host mesh / BSP / BVH built above. */
+int rt_upload_mesh_host(rt_ctx* ctx, const rt_mesh_host* m);
+int rt_upload_bsp_host(rt_ctx* ctx, const rt_bsp_host* b);
+int rt_upload_bvh_host(rt_ctx* ctx, const rt_bvh_host* b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RT02562_RT_H */

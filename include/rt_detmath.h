@@ -1,0 +1,126 @@
+/*
+ * rt_detmath.h -- the f32 transcendental functions this implementation pins.
+ *
+ * WGSL leaves the precision of sin/cos/acos implementation-defined (the
+ * reference's values come from naga 0.13 -> SPIR-V -> the Vulkan driver and
+ * are "parity unpinned").  One ulp of difference in
+ * setup_indirect (res/shaders/w7e3.wgsl:472-489) changes a path's next
+ * direction, so the HIP kernel and the CPU oracle must evaluate the SAME
+ * f32 operation sequence.  This header is that specification: Cody-Waite
+ * range reduction + minimax polynomials (Cephes single-precision
+ * coefficients), every operation an IEEE-754 binary32 add/mul/div/sqrt with
+ * round-to-nearest-even.  It must be compiled WITHOUT fp contraction
+ * (-ffp-contract=off) and without fast-math, with correctly rounded f32
+ * division/sqrt (clang HIP: -fhip-fp32-correctly-rounded-divide-sqrt).
+ *
+ * Included by the product kernels (C++/HIP) and by the C oracle.
+ */
+#ifndef RT02562_DETMATH_H
+#define RT02562_DETMATH_H
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define RT_HD __host__ __device__ static inline
+#else
+#define RT_HD static inline
+#endif
+
+#define RT_DET_PIF    3.14159265358979323846f   /* == f32 PI of the shaders */
+#define RT_DET_PIO2F  1.57079632679489661923f
+
+RT_HD float rt_det_sqrtf(float x) { return __builtin_sqrtf(x); }
+
+/* WGSL min/max/saturate/sign on f32 are implementation-defined for NaN and
+ * for the sign of zero; these are the pinned choices (ternaries, so the host
+ * libm and the GPU min/max instructions cannot disagree on +-0). */
+RT_HD float rt_minf(float a, float b) { return (b < a) ? b : a; }
+RT_HD float rt_maxf(float a, float b) { return (a < b) ? b : a; }
+RT_HD float rt_satf(float x) { return x > 0.0f ? (x < 1.0f ? x : 1.0f) : 0.0f; }
+RT_HD float rt_max0f(float x) { return x > 0.0f ? x : 0.0f; }
+RT_HD float rt_signf(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+RT_HD float rt_absf(float x) { return __builtin_fabsf(x); }
+
+/* Reduced-argument kernels on |x| <= pi/4 (z = x*x). */
+RT_HD float rt_det__sin_poly(float x, float z)
+{
+    return ((-1.9515295891E-4f * z + 8.3321608736E-3f) * z - 1.6666654611E-1f) * z * x + x;
+}
+RT_HD float rt_det__cos_poly(float z)
+{
+    return ((2.443315711809948E-5f * z - 1.388731625493765E-3f) * z + 4.166664568298827E-2f) * z * z
+           - 0.5f * z + 1.0f;
+}
+
+/* Cody-Waite reduction by pi/4 (three-part split of pi/4). Valid for |x| < 8192. */
+RT_HD float rt_det__reduce(float ax, int* octant)
+{
+    int j = (int)(1.27323954473516f * ax);
+    float y = (float)j;
+    if (j & 1) {
+        j += 1;
+        y += 1.0f;
+    }
+    *octant = j & 7;
+    return ((ax - y * 0.78515625f) - y * 2.4187564849853515625e-4f) - y * 3.77489497744594108e-8f;
+}
+
+RT_HD float rt_det_sinf(float x)
+{
+    int neg = 0;
+    float ax = x;
+    if (x < 0.0f) {
+        neg = 1;
+        ax = -x;
+    }
+    if (!(ax < 8192.0f)) return x - x;   /* NaN for inf/NaN/huge (never reached by the shaders) */
+    int j;
+    float r = rt_det__reduce(ax, &j);
+    if (j > 3) {
+        neg = !neg;
+        j -= 4;
+    }
+    float z = r * r;
+    float y = (j == 1 || j == 2) ? rt_det__cos_poly(z) : rt_det__sin_poly(r, z);
+    return neg ? -y : y;
+}
+
+RT_HD float rt_det_cosf(float x)
+{
+    float ax = x < 0.0f ? -x : x;
+    if (!(ax < 8192.0f)) return x - x;
+    int j;
+    float r = rt_det__reduce(ax, &j);
+    int neg = 0;
+    if (j > 3) {
+        j -= 4;
+        neg = 1;
+    }
+    if (j > 1) neg = !neg;
+    float z = r * r;
+    float y = (j == 1 || j == 2) ? rt_det__sin_poly(r, z) : rt_det__cos_poly(z);
+    return neg ? -y : y;
+}
+
+/* asin on |x| <= 0.5 */
+RT_HD float rt_det__asin_small(float x)
+{
+    float a = x < 0.0f ? -x : x;
+    if (a < 1.0e-4f) return x;
+    float z = x * x;
+    return ((((4.2163199048E-2f * z + 2.4181311049E-2f) * z + 4.5470025998E-2f) * z + 7.4953002686E-2f) * z
+            + 1.6666752422E-1f) * z * x + x;
+}
+
+RT_HD float rt_det_acosf(float x)
+{
+    if (x > 0.5f) {
+        float s = rt_det_sqrtf(0.5f * (1.0f - x));   /* NaN for x > 1 */
+        return 2.0f * rt_det__asin_small(s);
+    }
+    if (x < -0.5f) {
+        float s = rt_det_sqrtf(0.5f * (1.0f + x));
+        return RT_DET_PIF - 2.0f * rt_det__asin_small(s);
+    }
+    return RT_DET_PIO2F - rt_det__asin_small(x);  /* NaN propagates */
+}
+
+#endif /* RT02562_DETMATH_H */

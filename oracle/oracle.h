@@ -1,0 +1,152 @@
+/*
+ * oracle.h -- CPU restatement of cakarsubasi/02562_raytracer's hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load liboracle.so, and only as the checker
+ * (never as the thing measured or shipped).  The product (02562_raytracer_amd)
+ * never links or calls anything here.
+ *
+ * Parity pinning (see oracle/README.md): the reference (Rust + wgpu + WGSL) has
+ * no numeric golden vectors and cannot run in this container (no cargo, no
+ * Vulkan).  The restatement is pinned by (1) the reference's own structural
+ * tests (src/data_structures/bsp_tree.rs:356-420), (2) BSP topology fixtures
+ * produced by running the reference's instructor JavaScript BSP builder
+ * (js/bsp_tree/modules/BspTree_interleaved.js) under node, committed under
+ * tests/golden/ with the generating script, and (3) an independent numpy
+ * restatement of the triangle test.  Transcendentals follow include/rt_detmath.h
+ * (WGSL precision is implementation-defined: parity of those values vs the
+ * Vulkan driver is unpinned).
+ */
+#ifndef RT02562_ORACLE_H
+#define RT02562_ORACLE_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct or_material {   /* src/mesh.rs:12-20 */
+    float diffuse[4], ambient[4], specular[4];
+    uint32_t emissive, _pad[3];
+} or_material;
+
+typedef struct or_gpu_node {   /* src/data_structures/hlbvh.rs:508-515 */
+    float min[3];
+    uint32_t offset_ptr;
+    float max[3];
+    uint32_t n_prims;
+} or_gpu_node;
+
+typedef struct or_uniform {    /* src/bindings/uniform.rs:6-34 */
+    float camera_pos[3], camera_constant;
+    float camera_look_at[3], aspect_ratio;
+    float camera_up[3];
+    uint32_t selection1, selection2, subdivision_level, use_texture, iteration;
+    float uv_scale[2];
+    uint32_t resolution[2];
+} or_uniform;
+
+typedef struct or_scene {
+    const float* pos;          /* nverts x float4 */
+    const float* nrm;          /* nverts x float4 */
+    uint32_t nverts;
+    const uint32_t* idx;       /* ntris x uint4 */
+    uint32_t ntris;
+    const or_material* mats;
+    uint32_t nmats;
+    const uint32_t* lights;    /* [0] = sentinel */
+    uint32_t nlights;
+    /* BSP (src/bindings/bsp_tree.rs) */
+    const float* aabb;         /* 8 floats */
+    const uint32_t* tree;      /* nnodes x uint4 */
+    const float* planes;
+    uint32_t nnodes;
+    const uint32_t* ids;
+    uint32_t nids;
+    uint32_t max_depth;
+    /* BVH (src/bindings/bvh.rs) */
+    const or_gpu_node* bvh_nodes;
+    uint32_t bvh_nnodes;
+    const uint32_t* bvh_ids;
+    uint32_t bvh_nids;
+    float env[3];              /* constant environment for W9E1 escape */
+} or_scene;
+
+typedef struct or_counts {
+    uint64_t samples, primary, shadow, bounce;
+    uint64_t node_interior, node_leaf, bvh_pops, ids_read, tri_tests, tri_accepts;
+} or_counts;
+
+enum { OR_MODE_W1E6 = 0, OR_MODE_W6E1 = 1, OR_MODE_PROJECT = 2, OR_MODE_W7E3 = 3, OR_MODE_W9E1 = 4 };
+enum { OR_TRAV_BSP = 0, OR_TRAV_BVH = 1, OR_TRAV_NONE = 2 };
+
+/* ---- mesh ---- */
+typedef struct or_mesh {
+    float* pos;       /* nverts x 4 */
+    float* nrm;       /* nverts x 4 */
+    uint32_t* idx;    /* ntris x 4 */
+    or_material* mats;
+    uint32_t* lights;
+    uint32_t nverts, ntris, nmats, nlights;
+} or_mesh;
+
+/* Mesh::from_obj (src/mesh.rs:78-202) with tobj 4.0 load options
+ * {single_index, triangulate}; returns 0 on success. */
+int or_load_obj(const char* path, or_mesh* out);
+/* light list of StorageMeshGpu (src/bindings/storage_mesh.rs:316-332): caller frees */
+int or_light_list(const uint32_t* idx, uint32_t ntris, const or_material* mats, uint32_t nmats,
+                  uint32_t** out, uint32_t* nout);
+void or_free_mesh(or_mesh* m);
+
+/* ---- BSP (src/data_structures/bsp_tree.rs) ---- */
+typedef struct or_bsp {
+    uint32_t* tree;   /* nnodes x 4 */
+    float* planes;
+    uint32_t* ids;
+    float aabb[8];
+    uint32_t nnodes, nids, max_depth;
+} or_bsp;
+int or_bsp_build(const float* pos, uint32_t nverts, const uint32_t* idx, uint32_t ntris,
+                 uint32_t max_depth, uint32_t max_leaf, or_bsp* out);
+void or_free_bsp(or_bsp* b);
+/* The same builder with the instructor JavaScript's f64 arithmetic
+ * (js/bsp_tree/modules/BspTree_interleaved.js:28-188); used only to pin the
+ * restatement against fixtures produced by running that JavaScript. */
+int or_bsp_build_js64(const float* pos, uint32_t nverts, const uint32_t* idx, uint32_t ntris,
+                      uint32_t max_depth, uint32_t max_leaf, or_bsp* out);
+
+/* ---- HLBVH (src/data_structures/hlbvh.rs) ---- */
+typedef struct or_bvh {
+    or_gpu_node* nodes;
+    uint32_t* tri_ids;
+    uint32_t nnodes, nids;
+} or_bvh;
+int or_bvh_build(const float* pos, uint32_t nverts, const uint32_t* idx, uint32_t ntris,
+                 uint32_t max_prims, or_bvh* out);
+void or_free_bvh(or_bvh* b);
+
+/* ---- render: the fs_main grid of the scene shader over a region ----
+ * accum: w*h float4 in/out (read when first_iter > 0); ids: w*h or NULL. */
+int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int mode, int trav,
+              uint32_t x0, uint32_t y0, uint32_t w, uint32_t h,
+              uint32_t first_iter, uint32_t spp, float* accum, uint32_t* ids,
+              or_counts* counts, int nthreads);
+
+/* single closest-hit query through the BSP/BVH (intersect_trimesh), for tests:
+ * returns 1 on hit, writes tri index and distance. */
+int or_trace_one(const or_scene* s, int trav, int face_normals, const float o[3], const float d[3],
+                 float tmin, float tmax, uint32_t* tri, float* dist);
+
+/* brute-force closest hit over all triangles (w5e2-style loop, no accel). */
+int or_trace_brute(const or_scene* s, const float o[3], const float d[3], float tmin, float tmax,
+                   uint32_t* tri, float* dist);
+
+/* math used by the self tests */
+float or_det_sinf(float x);
+float or_det_cosf(float x);
+float or_det_acosf(float x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
