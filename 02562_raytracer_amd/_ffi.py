@@ -24,6 +24,7 @@ RT_MODE_W1E6, RT_MODE_W6E1, RT_MODE_PROJECT, RT_MODE_W7E3, RT_MODE_W9E1 = range(
 RT_TRAVERSE_BSP, RT_TRAVERSE_BVH, RT_TRAVERSE_NONE = range(3)
 RT_OPT_DETAIL_COUNTERS = 1
 RT_OPT_WAVES_PER_CU = 2
+RT_OPT_SHADE_THRESHOLD = 3
 
 MODES = {"W1E6": RT_MODE_W1E6, "W6E1": RT_MODE_W6E1, "PROJECT": RT_MODE_PROJECT, "W7E3": RT_MODE_W7E3,
          "W9E1": RT_MODE_W9E1}
@@ -61,7 +62,7 @@ class Tileset(C.Structure):
 
 
 COUNT_FIELDS = ["samples", "primary", "shadow", "bounce", "node_interior", "node_leaf", "bvh_pops",
-                "ids_read", "tri_tests", "tri_accepts"]
+                "ids_read", "tri_tests", "tri_accepts", "trips", "lane_steps", "leaf_iters"]
 
 
 class RayCounts(C.Structure):

@@ -55,6 +55,7 @@ struct rt_ctx {
     std::string err;
     int num_cus = 256;
     int waves_per_cu = 16;
+    int shade_threshold = 16;
     bool detail = false;
     // host copies needed to build the triangle records on BSP/BVH upload
     std::vector<float> h_pos;
@@ -232,6 +233,10 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
     case RT_OPT_WAVES_PER_CU:
         if (value < 1 || value > 32) return fail(c, RT_E_INVALID, "waves per CU must be in [1,32]");
         c->waves_per_cu = (int)value;
+        return RT_OK;
+    case RT_OPT_SHADE_THRESHOLD:
+        if (value < 0 || value > 64) return fail(c, RT_E_INVALID, "shade threshold must be in [0,64] (64 = lockstep)");
+        c->shade_threshold = (int)value;
         return RT_OK;
     default:
         return fail(c, RT_E_INVALID, "unknown option");
@@ -511,9 +516,11 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     S.bvh_ids = c->bvh_ids.as<uint32_t>();
     S.bvh_nnodes = c->bvh_nnodes;
     L.u = c->u;
+    rtk::camera_basis(c->u, L.cam);
     L.jitter = c->has_jitter ? c->jitter.as<float>() : nullptr;
     memcpy(L.env, c->env, sizeof L.env);
     L.work_counter = c->work.as<uint32_t>();
+    L.shade_threshold = (uint32_t)c->shade_threshold;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->work.p, 0, 64, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 16 * sizeof(unsigned long long), c->stream));

@@ -34,6 +34,7 @@ struct DevScene {
 // Work mapping + outputs of one launch.
 struct DevLaunch {
     rt_uniform u;
+    float cam[14];                // camera basis e, v, b1, b2, d, aspect (get_camera_ray, w7e3.wgsl:211-228)
     const float* jitter;          // subdiv^2 float2 (device), may be null when subdiv == 1
     float env[3];
     // region mode (tileset == 0): 8x8 tiles over [x0,x0+w) x [y0,y0+h), row-major region output
@@ -44,6 +45,7 @@ struct DevLaunch {
     uint32_t tiles_x, tiles_y;    // tile grid (of the region, or of the frame)
     uint32_t nwork;               // work items (tiles) in this launch
     uint32_t first_iter, spp;
+    uint32_t shade_threshold;     // k_path: shade when <= this many lanes still trace
     float4* accum;
     uint32_t* ids;
     uint32_t* work_counter;       // zeroed before launch
@@ -59,6 +61,9 @@ int launch_unpack(uint32_t width, uint32_t height, uint32_t nranks, uint32_t loc
                   uint32_t* frame_ids, hipStream_t stream);
 
 int launch_selftest_math(const float* in, float* out, uint32_t n, hipStream_t stream);
+
+// get_camera_ray's basis from the uniforms (host, same f32 operations as the shader)
+void camera_basis(const rt_uniform& u, float cam[14]);
 
 // Host reference of the pinned math for the self test (same header, host compile).
 void host_math(const float* in, float* out, uint32_t n);

@@ -69,15 +69,17 @@ __device__ __forceinline__ uint32_t mcg31(uint32_t& prev)
 __device__ __forceinline__ float rnd(uint32_t& prev) { return (float)mcg31(prev) / (float)0x80000000u; }
 
 // ------------------------------------------------------------------ counters
-enum { C_SAMPLES, C_PRIMARY, C_SHADOW, C_BOUNCE, C_INTERIOR, C_LEAF, C_POPS, C_IDS, C_TESTS, C_ACCEPTS, C_N };
+enum { C_SAMPLES, C_PRIMARY, C_SHADOW, C_BOUNCE, C_INTERIOR, C_LEAF, C_POPS, C_IDS, C_TESTS, C_ACCEPTS,
+       C_TRIPS, C_LANE_STEPS, C_LEAF_ITERS, C_N };
 
 struct Counters {
     uint32_t v[C_N];
+    uint32_t leafc;   // diagnostics: triangles in the leaf this lane visited this trip
 };
 
 __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* out, bool detail)
 {
-    const int n = detail ? C_N : 4;
+    const int n = detail ? (int)C_N : 4;
     for (int i = 0; i < n; i++) {
         uint32_t x = c.v[i];
         unsigned long long s = x;
@@ -92,16 +94,18 @@ struct Cam {
     f3 e, v, b1, b2;
     float d, aspect;
 };
-__device__ __forceinline__ Cam make_cam(const rt_uniform& u)
+// The basis v = normalize(p - e), b1 = normalize(cross(v, u)), b2 = cross(b1, v)
+// is loop-invariant: rt_api.cpp evaluates it once on the host with the same
+// IEEE operations (no contraction) and passes it as kernel arguments (SGPRs).
+__device__ __forceinline__ Cam make_cam(const DevLaunch& L)
 {
     Cam c;
-    c.e = ld3(u.camera_pos);
-    f3 p = ld3(u.camera_look_at), up = ld3(u.camera_up);
-    c.v = normalize(sub(p, c.e));
-    c.d = u.camera_constant;
-    c.aspect = u.aspect_ratio;
-    c.b1 = normalize(cross(c.v, up));
-    c.b2 = cross(c.b1, c.v);
+    c.e = ld3(L.cam + 0);
+    c.v = ld3(L.cam + 3);
+    c.b1 = ld3(L.cam + 6);
+    c.b2 = ld3(L.cam + 9);
+    c.d = L.cam[12];
+    c.aspect = L.cam[13];
     return c;
 }
 __device__ __forceinline__ f3 cam_dir(const Cam& c, float ux, float uy, float jx, float jy)
@@ -150,6 +154,23 @@ __device__ __forceinline__ void pixel_uv(const rt_uniform& u, uint32_t x, uint32
 // ------------------------------------------------------------------ triangle test
 // intersect_triangle_indexed (w7e3.wgsl:286-332) on a pre-transformed record:
 // r0 = (v0.xyz, e0.x), r1 = (e0.yz, e1.xy), r2 = (e1.z, n.xyz).
+//
+// Exact fast rejection: the accept predicate is a pure function of the
+// correctly rounded quotients beta = a/denom, gamma = b/denom, dist = c/denom,
+// so a quotient is only divided out when its sign/range is not already
+// certain.  RN(a/denom) < 0  <=>  a != 0, sign(a) != sign(denom) and the
+// quotient does not underflow to -0; with 2^-60 <= |a| and |denom| <= 2^60
+// the quotient is >= 2^-120 in magnitude, far from the 2^-150 underflow
+// threshold, so the sign test is exact there (anything else falls back to
+// the division).  The dist range test uses v_rcp_f32 (<= 1 ulp) with a
+// 2^-20 relative margin, which bounds |RN(c*rcp(denom)) - RN(c/denom)|.
+__device__ __forceinline__ bool sign_certain_neg(float a, float den)
+{
+    return a != 0.0f && rt_absf(a) >= 0x1p-60f && ((__float_as_uint(a) ^ __float_as_uint(den)) >> 31);
+}
+__device__ __forceinline__ bool sign_uncertain(float a) { return a != 0.0f && !(rt_absf(a) >= 0x1p-60f); }
+
+template <bool FAST>
 __device__ __forceinline__ bool tri_test(const float4* recs, uint32_t k, f3 o, f3 w, float tmin, float tmax,
                                          float& dist, float& beta, float& gamma)
 {
@@ -160,9 +181,18 @@ __device__ __forceinline__ bool tri_test(const float4* recs, uint32_t k, f3 o, f
     const f3 nom = cross(ov, w);
     const float denom = dot(w, n);
     if (rt_absf(denom) < 1e-10f) return false;
-    beta = dot(nom, e1) / denom;
-    gamma = -dot(nom, e0) / denom;
-    dist = dot(ov, n) / denom;
+    const float a = dot(nom, e1);
+    const float b = -dot(nom, e0);
+    const float c = dot(ov, n);
+    if (FAST && rt_absf(denom) <= 0x1p60f) {
+        if (sign_certain_neg(a, denom) || sign_certain_neg(b, denom)) return false;
+        const float tq = c * __builtin_amdgcn_rcpf(denom);
+        const float m = rt_absf(tq) * 0x1p-20f + 1e-30f;
+        if (tq - m > tmax || tq + m < tmin) return false;
+    }
+    beta = a / denom;
+    gamma = b / denom;
+    dist = c / denom;
     return !(beta < 0.0f || gamma < 0.0f || beta + gamma > 1.0f || dist > tmax || dist < tmin);
 }
 
@@ -171,76 +201,134 @@ struct TraceOut {
     float beta, gamma, dist;
 };
 
-// ------------------------------------------------------------------ BSP traversal
-// intersect_trimesh, bsp.wgsl:10-81.  The explicit stack keeps {far node, t};
-// the tmax a pop restores is the t of the entry below it (or the ray's
-// original tmax), which is exactly the value bsp.wgsl saves in branch_ray.y.
-// anyhit: stop at the first accepted triangle (shadow rays only need the
-// boolean; the walk up to that triangle is identical, so the result is too).
-template <bool COUNT>
-__device__ __forceinline__ bool trace_bsp(const DevScene& S, uint2* stk, const f3 o, const f3 d, float tmin,
-                                          float tmax, const bool anyhit, TraceOut& out, Counters& c)
+// Per-lane traversal state (kept in registers across the persistent loop).
+struct Trav {
+    uint32_t node;   // BSP: current node      BVH: stack top
+    uint32_t lvl;    // BSP: stack depth       BVH: pops so far
+    uint32_t leaf_k, leaf_end;   // triangle slots of the leaf being tested (empty when equal)
+    float tmin, tmax, tmax0;
+    bool found;
+    TraceOut best;
+};
+
+__device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
 {
-    const float tmax0 = tmax;
-    uint32_t node = 0, lvl = 0;
-    for (uint32_t guard = 0; guard < (1u << 24); guard++) {
-        const uint2 n = S.bsp_nodes[node];
+    t.node = 0;
+    t.lvl = 0;
+    t.leaf_k = t.leaf_end = 0;
+    t.tmin = tmin;
+    t.tmax = tmax;
+    t.tmax0 = tmax;
+    t.found = false;
+}
+
+// One triangle test of the current leaf (shared by BSP and BVH).
+template <bool COUNT>
+__device__ __forceinline__ void leaf_test(const float4* recs, const f3 o, const f3 d, Trav& t, Counters& c)
+{
+    if (COUNT) {
+        c.v[C_IDS]++;
+        c.v[C_TESTS]++;
+    }
+    float dist, beta, gamma;
+    if (tri_test<true>(recs, t.leaf_k, o, d, t.tmin, t.tmax, dist, beta, gamma)) {
+        if (COUNT) c.v[C_ACCEPTS]++;
+        t.tmax = dist;
+        t.found = true;
+        t.best.k = t.leaf_k;
+        t.best.beta = beta;
+        t.best.gamma = gamma;
+        t.best.dist = dist;
+    }
+    t.leaf_k++;
+}
+
+// ------------------------------------------------------------------ BSP traversal
+// intersect_trimesh, bsp.wgsl:10-81, as a per-lane state machine: each call
+// visits at most one node and tests at most one triangle ("if-if"), so a wave
+// trip never serialises behind the longest leaf of any lane.  Returns true
+// when the ray is finished (t.found = hit).  The explicit stack keeps
+// {far node, t}; the tmax a pop restores is the t of the entry below it (or
+// the ray's original tmax): exactly the value bsp.wgsl saves in branch_ray.y
+// (tmax only changes on push, pop, and on an accept, after which the walk ends).
+// anyhit: stop at the first accepted triangle -- shadow rays use only the
+// boolean, and the walk up to that triangle is identical, so it is too.
+// Interior nodes: the exact t = RN((plane - o)/denom) is only divided out when
+// the approximate t (v_rcp_f32, 2^-20 margin) cannot decide near/far.
+__device__ __forceinline__ bool bsp_pop(uint2* stk, Trav& t)
+{
+    if (t.lvl == 0) return true;   // `branch_lvl == 0u` -> return false (miss)
+    t.lvl--;
+    const uint2 e = stk[t.lvl * 256u];
+    t.node = e.x;
+    t.tmin = __uint_as_float(e.y);
+    t.tmax = t.lvl ? __uint_as_float(stk[(t.lvl - 1u) * 256u].y) : t.tmax0;
+    return false;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool bsp_step(const DevScene& S, uint2* stk, const f3 o, const f3 d, const f3 inv,
+                                         bool anyhit, Trav& t, Counters& c)
+{
+    if (t.leaf_k == t.leaf_end) {
+        const uint2 n = S.bsp_nodes[t.node];
         const uint32_t axis = n.x & 3u;
         if (axis == 3u) {
             if (COUNT) c.v[C_LEAF]++;
-            const uint32_t count = n.x >> 2, first = n.y;
-            bool found = false;
-            for (uint32_t j = 0; j < count; j++) {
-                if (COUNT) {
-                    c.v[C_IDS]++;
-                    c.v[C_TESTS]++;
-                }
-                float dist, beta, gamma;
-                if (tri_test(S.bsp_recs, first + j, o, d, tmin, tmax, dist, beta, gamma)) {
-                    if (COUNT) c.v[C_ACCEPTS]++;
-                    tmax = dist;
-                    found = true;
-                    out.k = first + j;
-                    out.beta = beta;
-                    out.gamma = gamma;
-                    out.dist = dist;
-                    if (anyhit) break;
+            const uint32_t count = n.x >> 2;
+            if (COUNT) c.leafc = count;
+            if (count == 0u) return bsp_pop(stk, t);
+            t.leaf_k = n.y;
+            t.leaf_end = n.y + count;
+        } else {
+            if (COUNT) c.v[C_INTERIOR]++;
+            const float ad = comp(d, axis), ao = comp(o, axis);
+            const uint32_t left = 2u * t.node + 1u;
+            const uint32_t near_node = ad >= 0.0f ? left : left + 1u;
+            const uint32_t far_node = ad >= 0.0f ? left + 1u : left;
+            const float x = __uint_as_float(n.y) - ao;
+            const float tq = x * comp(inv, axis);
+            const float m = rt_absf(tq) * 0x1p-20f + 1e-30f;
+            if (tq - m > t.tmax) {   // certainly t > tmax
+                t.node = near_node;
+            } else if (tq + m < t.tmin && tq + m <= t.tmax) {   // certainly !(t > tmax) && t < tmin
+                t.node = far_node;
+            } else {
+                const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
+                const float tt = x / denom;
+                if (tt > t.tmax) {
+                    t.node = near_node;
+                } else if (tt < t.tmin) {
+                    t.node = far_node;
+                } else {
+                    stk[t.lvl * 256u] = make_uint2(far_node, __float_as_uint(tt));
+                    t.lvl++;
+                    t.tmax = tt;
+                    t.node = near_node;
                 }
             }
-            if (found) return true;
-            if (lvl == 0) return false;
-            lvl--;
-            const uint2 e = stk[lvl * 256u];
-            node = e.x;
-            tmin = __uint_as_float(e.y);
-            tmax = lvl ? __uint_as_float(stk[(lvl - 1u) * 256u].y) : tmax0;
-            continue;
-        }
-        if (COUNT) c.v[C_INTERIOR]++;
-        const float ad = comp(d, axis), ao = comp(o, axis);
-        const uint32_t left = 2u * node + 1u;
-        const uint32_t near_node = ad >= 0.0f ? left : left + 1u;
-        const uint32_t far_node = ad >= 0.0f ? left + 1u : left;
-        const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
-        const float t = (__uint_as_float(n.y) - ao) / denom;
-        if (t > tmax) {
-            node = near_node;
-        } else if (t < tmin) {
-            node = far_node;
-        } else {
-            stk[lvl * 256u] = make_uint2(far_node, __float_as_uint(t));
-            lvl++;
-            tmax = t;
-            node = near_node;
+            return false;
         }
     }
-    return false;
+    leaf_test<COUNT>(S.bsp_recs, o, d, t, c);
+    if (t.found && anyhit) t.leaf_k = t.leaf_end;
+    if (t.leaf_k != t.leaf_end) return false;
+    if (t.found) return true;   // a leaf with an accepted triangle ends the walk
+    return bsp_pop(stk, t);
+}
+
+// 1/denom per axis for the approximate interior-node test (denom as bsp.wgsl:63)
+__device__ __forceinline__ f3 bsp_inv(const f3 d)
+{
+    return V(__builtin_amdgcn_rcpf(rt_absf(d.x) < 1.0e-8f ? 1.0e-8f : d.x),
+             __builtin_amdgcn_rcpf(rt_absf(d.y) < 1.0e-8f ? 1.0e-8f : d.y),
+             __builtin_amdgcn_rcpf(rt_absf(d.z) < 1.0e-8f ? 1.0e-8f : d.z));
 }
 
 // ------------------------------------------------------------------ BVH traversal
 // intersect_bvh + intersect_bb2, bvh.wgsl:154-191 / 16-83: slab test in axis
 // order y, x, z on [0, 1e27] (ray interval ignored), right child popped first,
-// 1000-pop cap, WGSL index clamping of the 50-entry stack.
+// 1000-pop cap, WGSL index clamping of the 50-entry stack.  One pop per call.
 __device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, const float4 b)
 {
     float t0 = 0.0f, t1 = 1e27f;
@@ -263,58 +351,80 @@ __device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, co
     return !(t0 > t1);
 }
 
-template <bool COUNT>
-__device__ __forceinline__ bool trace_bvh(const DevScene& S, uint32_t* stk, const f3 o, const f3 d, float tmin,
-                                          float tmax, const bool anyhit, TraceOut& out, Counters& c)
+__device__ __forceinline__ void bvh_init(Trav& t, uint32_t* stk, float tmin, float tmax)
 {
-    const f3 inv = V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    uint32_t top = 0;
-    stk[0] = 0u;
-    top = 1;
-    bool found = false;
-    for (uint32_t pops = 0; pops < 1000u && top > 0u; pops++) {
-        top--;
-        const uint32_t cur = stk[(top < 50u ? top : 49u) * 256u];
+    trav_init(t, tmin, tmax);
+    stk[0] = 0u;   // stack_push_node(0u)
+    t.node = 1;    // top
+    t.lvl = 0;     // pops
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const f3 o, const f3 d, const f3 inv,
+                                         bool anyhit, Trav& t, Counters& c)
+{
+    if (t.leaf_k == t.leaf_end) {
+        if (t.lvl >= 1000u || t.node == 0u) return true;
+        t.lvl++;
+        t.node--;
+        const uint32_t cur = stk[(t.node < 50u ? t.node : 49u) * 256u];
         if (COUNT) c.v[C_POPS]++;
         const float4 a = S.bvh_nodes[2u * cur], b = S.bvh_nodes[2u * cur + 1u];
         if (bb2(inv, o, a, b)) {
             const uint32_t off = __float_as_uint(a.w), np = __float_as_uint(b.w);
+            if (COUNT) c.leafc = np;
             if (np > 0u) {
-                for (uint32_t i = 0; i < np; i++) {
-                    if (COUNT) {
-                        c.v[C_IDS]++;
-                        c.v[C_TESTS]++;
-                    }
-                    float dist, beta, gamma;
-                    if (tri_test(S.bvh_recs, off + i, o, d, tmin, tmax, dist, beta, gamma)) {
-                        if (COUNT) c.v[C_ACCEPTS]++;
-                        tmax = dist;
-                        found = true;
-                        out.k = off + i;
-                        out.beta = beta;
-                        out.gamma = gamma;
-                        out.dist = dist;
-                        if (anyhit) return true;
-                    }
-                }
+                t.leaf_k = off;
+                t.leaf_end = off + np;
             } else {
-                stk[(top < 50u ? top : 49u) * 256u] = cur + 1u;
-                top++;
-                stk[(top < 50u ? top : 49u) * 256u] = off;
-                top++;
+                stk[(t.node < 50u ? t.node : 49u) * 256u] = cur + 1u;
+                t.node++;
+                stk[(t.node < 50u ? t.node : 49u) * 256u] = off;
+                t.node++;
             }
         }
+        if (t.leaf_k == t.leaf_end) return t.lvl >= 1000u || t.node == 0u;
     }
-    return found;
+    leaf_test<COUNT>(S.bvh_recs, o, d, t, c);
+    if (t.found && anyhit) return true;
+    if (t.leaf_k != t.leaf_end) return false;
+    return t.lvl >= 1000u || t.node == 0u;
 }
 
+// The 1/d of bvh.wgsl:155 (exact division: it feeds the slab test directly).
+__device__ __forceinline__ f3 bvh_inv(const f3 d) { return V(1.0f / d.x, 1.0f / d.y, 1.0f / d.z); }
+
+template <int TRAV>
+__device__ __forceinline__ f3 trav_inv(const f3 d)
+{
+    return TRAV == RT_TRAVERSE_BVH ? bvh_inv(d) : bsp_inv(d);
+}
+template <int TRAV>
+__device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float tmax)
+{
+    if (TRAV == RT_TRAVERSE_BVH) bvh_init(t, reinterpret_cast<uint32_t*>(stk), tmin, tmax);
+    else trav_init(t, tmin, tmax);
+}
+template <int TRAV, bool COUNT>
+__device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const f3 o, const f3 d, const f3 inv,
+                                          bool anyhit, Trav& t, Counters& c)
+{
+    if (TRAV == RT_TRAVERSE_BVH) return bvh_step<COUNT>(S, reinterpret_cast<uint32_t*>(stk), o, d, inv, anyhit, t, c);
+    return bsp_step<COUNT>(S, reinterpret_cast<uint2*>(stk), o, d, inv, anyhit, t, c);
+}
+
+// Whole traversal of one ray (used by the primary-ray kernel).
 template <int TRAV, bool COUNT>
 __device__ __forceinline__ bool trace(const DevScene& S, void* stk, const f3 o, const f3 d, float tmin, float tmax,
                                       bool anyhit, TraceOut& out, Counters& c)
 {
-    if (TRAV == RT_TRAVERSE_BVH)
-        return trace_bvh<COUNT>(S, reinterpret_cast<uint32_t*>(stk), o, d, tmin, tmax, anyhit, out, c);
-    return trace_bsp<COUNT>(S, reinterpret_cast<uint2*>(stk), o, d, tmin, tmax, anyhit, out, c);
+    Trav t;
+    trav_start<TRAV>(t, stk, tmin, tmax);
+    const f3 inv = trav_inv<TRAV>(d);
+    for (uint32_t guard = 0; guard < (1u << 24); guard++)
+        if (trav_step<TRAV, COUNT>(S, stk, o, d, inv, anyhit, t, c)) break;
+    out = t.best;
+    return t.found;
 }
 
 // Hit record of the accepted triangle (the values intersect_triangle_indexed
@@ -409,6 +519,22 @@ __device__ __forceinline__ Light sample_area_light(const DevScene& S, f3 pos, ui
 enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 
 // ------------------------------------------------------------------ W7E3 / W9E1 path kernel
+// Persistent "while-while" megakernel with per-lane work regeneration:
+//   * every lane owns one pixel and runs its `spp` iterations in order; a lane
+//     whose pixel is finished takes the next pixel slot from the global queue
+//     (wave-aggregated: one atomic per refill, slots handed out with
+//     ballot + mbcnt prefix ranks, so idle lanes are compacted onto new work);
+//   * traversal phase: each loop trip advances every tracing lane by one BSP
+//     node / BVH pop; lanes whose ray finished wait;
+//   * shading phase: entered when at most `shade_threshold` lanes are still
+//     tracing (or none): the finished lanes shade, set up their next ray
+//     (shadow, bounce or the next sample) and rejoin; lanes still mid-ray keep
+//     their traversal state, so no lane waits for the slowest ray of the wave.
+// The per-pixel arithmetic is exactly fs_main (w7e3.wgsl:233-272 /
+// w9e1.wgsl:244-284): the lambertian continuation after the shadow ray only
+// needs the two possible contributions (visible / blocked), the RR decision
+// and the next direction, all computed with the same operations in the same
+// PRNG order before the shadow ray is traced.
 template <int MODE, int TRAV, bool COUNT>
 __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
 {
@@ -418,72 +544,82 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
     constexpr bool W9 = MODE == RT_MODE_W9E1;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
-    const Cam cam = make_cam(L.u);
+    const Cam cam = make_cam(L);
     const float fH = (float)L.u.resolution[1];
+    const uint32_t resx = L.u.resolution[0];
     const uint32_t light_tris = S.nlights - 1u;
     const uint32_t sel = W9 ? L.u.selection1 : 0u;
+    const uint32_t it_end = L.first_iter + L.spp;
+    const uint32_t nslots = L.nwork * 64u;
+    const uint32_t T = L.shade_threshold;
+    const f3 env = V(L.env[0], L.env[1], L.env[2]);
     Counters cnt;
 #pragma unroll
     for (int i = 0; i < C_N; i++) cnt.v[i] = 0;
 
+    bool alive = false, tracing = false, exhausted = L.spp == 0u, shadow = false, emit = true, survive = false;
+    uint32_t px = 0, py = 0, out = 0, it = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
+    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+    f3 res = V(0, 0, 0), fac = V(1, 1, 1), ro = V(0, 0, 0), rd = V(0, 0, 1), inv = V(0, 0, 0);
+    f3 ndir = V(0, 0, 1), cu = V(0, 0, 0), cb = V(0, 0, 0);
+    Trav tr;
+    trav_init(tr, 0.0f, 0.0f);
+
+    // fs_main prologue for iteration `it` of the lane's pixel (w7e3.wgsl:236-248)
+    auto start_sample = [&]() {
+        rng = tea16(py * resx + px, it);
+        float jx = rnd(rng);
+        float jy = rnd(rng);
+        jx = jx / fH;
+        jy = jy / fH;
+        float ux, uy;
+        pixel_uv(L.u, px, py, ux, uy);
+        rd = cam_dir(cam, ux, uy, jx, jy);
+        ro = cam.e;
+        res = V(0, 0, 0);
+        fac = V(1, 1, 1);
+        emit = true;
+        bounce = 0;
+        prim = 0xFFFFFFFFu;
+        shadow = false;
+        inv = trav_inv<TRAV>(rd);
+        trav_start<TRAV>(tr, stk, ETA, 5000.0f);
+        tracing = true;
+        cnt.v[C_SAMPLES]++;
+        cnt.v[C_PRIMARY]++;
+    };
+
     for (;;) {
-        const uint32_t work = fetch_work(L.work_counter, lane);
-        if (work >= L.nwork) break;
-        const Pix px = map_pixel(L, work, lane);
-        bool alive = px.valid && L.spp > 0u;
-        uint32_t it = L.first_iter;
-        const uint32_t it_end = L.first_iter + L.spp;
-        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
-        if (alive && L.first_iter > 0u) {
-            const float4 pa = L.accum[px.out];
-            a0 = pa.x;
-            a1 = pa.y;
-            a2 = pa.z;
-        }
-        uint32_t prim = 0xFFFFFFFFu, rng = 0, phase = PH_NEW, bounce = 0;
-        bool emit = true, survive = false;
-        f3 res = V(0, 0, 0), fac = V(1, 1, 1);
-        f3 ro = V(0, 0, 0), rd = V(0, 0, 1);
-        float rtmin = 0.0f, rtmax = 0.0f, prob = 1.0f;
-        f3 hpos = V(0, 0, 0), hnrm = V(0, 0, 1), dvf = V(0, 0, 0), zf = V(0, 0, 0), amb = V(0, 0, 0);
-
-        while (__ballot(alive)) {
-            if (alive && phase == PH_NEW) {
-                // fs_main prologue, w7e3.wgsl:236-248
-                const uint32_t launch_idx = px.y * L.u.resolution[0] + px.x;
-                rng = tea16(launch_idx, it);
-                float jx = rnd(rng);
-                float jy = rnd(rng);
-                jx = jx / fH;
-                jy = jy / fH;
-                float ux, uy;
-                pixel_uv(L.u, px.x, px.y, ux, uy);
-                rd = cam_dir(cam, ux, uy, jx, jy);
-                ro = cam.e;
-                rtmin = ETA;
-                rtmax = 5000.0f;
-                res = V(0, 0, 0);
-                fac = V(1, 1, 1);
-                emit = true;
-                bounce = 0;
-                prim = 0xFFFFFFFFu;
-                phase = PH_CLOSEST;
-                cnt.v[C_SAMPLES]++;
-                cnt.v[C_PRIMARY]++;
+        const uint64_t trm = __ballot(alive && tracing);
+        const uint64_t wtm = __ballot(alive && !tracing);
+        if (trm != 0 && (wtm == 0 || T >= 64u || (uint32_t)__popcll(trm) > T)) {
+            // ---- traversal phase: one node per tracing lane
+            if (COUNT) cnt.leafc = 0;
+            if (alive && tracing) {
+                if (COUNT) cnt.v[C_LANE_STEPS]++;
+                if (trav_step<TRAV, COUNT>(S, stk, ro, rd, inv, shadow, tr, cnt)) tracing = false;
             }
-            TraceOut tr;
-            bool hit = false;
-            if (alive) hit = trace<TRAV, COUNT>(S, stk, ro, rd, rtmin, rtmax, phase == PH_SHADOW, tr, cnt);
-            if (!alive) continue;
-
+            if (COUNT) {
+                uint32_t mx = cnt.leafc;
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+                if (lane == 0) {
+                    cnt.v[C_TRIPS]++;
+                    cnt.v[C_LEAF_ITERS] += mx;
+                }
+            }
+            continue;
+        }
+        // ---- shading phase
+        if (alive && !tracing) {
             bool sample_done = false;
-            if (phase == PH_CLOSEST) {
-                if (hit) {
-                    const HitRec h = resolve<TRAV>(S, tr, ro, rd, !W9);
+            if (!shadow) {
+                if (tr.found) {
+                    const HitRec h = resolve<TRAV>(S, tr.best, ro, rd, !W9);
                     if (bounce == 0) prim = h.tri;
                     const rt_material& m = mat_of(S, h.material);
                     if (sel == 0u) {
-                        // lambertian (w7e3.wgsl:427-470 / w9e1.wgsl:428-470) up to the shadow ray
+                        // lambertian (w7e3.wgsl:427-470 / w9e1.wgsl:428-470)
                         const f3 brdf = divs(ld3(m.diffuse), RT_PI_F);
                         const f3 emission = ld3(m.ambient);
                         Light Lt;
@@ -493,36 +629,39 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
                             Lt.dist = 999999.0f;
                         } else {
                             const uint32_t ri = mcg31(rng);
-                            const uint32_t idx = ri % light_tris + 1u;
-                            Lt = sample_area_light(S, h.pos, idx, rng);
+                            Lt = sample_area_light(S, h.pos, ri % light_tris + 1u, rng);
                         }
                         f3 dv = mul(muls(brdf, rt_satf(dot(h.nrm, Lt.w_i))), Lt.l_i);
                         if (!W9) dv = muls(dv, (float)light_tris);
-                        amb = emit ? (W9 ? mul(emission, fac) : emission) : V(0, 0, 0);
-                        dvf = mul(dv, fac);
-                        zf = mul(V(0, 0, 0), fac);
+                        const f3 amb = emit ? (W9 ? mul(emission, fac) : emission) : V(0, 0, 0);
+                        cu = add(mul(dv, fac), amb);             // not blocked: diffuse*factor + ambient
+                        cb = add(mul(V(0, 0, 0), fac), amb);     // blocked: vec3(0)*factor + ambient
                         fac = mul(fac, muls(brdf, RT_PI_F));
-                        prob = (brdf.x + brdf.y + brdf.z) / 3.0f;
+                        const float prob = (brdf.x + brdf.y + brdf.z) / 3.0f;
                         survive = rnd(rng) < prob;
-                        hpos = h.pos;
-                        hnrm = h.nrm;
-                        // shadow ray (ray_init + tmin/tmax override)
+                        if (survive && bounce + 1u < 50u) {
+                            ndir = indirect_dir(h.nrm, rng);   // setup_indirect (:472-489)
+                            fac = divs(fac, prob);
+                        }
+                        // shadow ray (ray_init + tmin/tmax override, :442-449)
                         ro = h.pos;
                         rd = Lt.w_i;
-                        rtmin = ETA;
-                        rtmax = Lt.dist - ETA;
-                        phase = PH_SHADOW;
+                        inv = trav_inv<TRAV>(rd);
+                        trav_start<TRAV>(tr, stk, ETA, Lt.dist - ETA);
+                        shadow = true;
+                        tracing = true;
                         cnt.v[C_SHADOW]++;
                     } else if (sel == 2u) {
                         // mirror (w9e1.wgsl:491-504): reflect, offset origin, emit = true
                         const f3 n = h.nrm;
                         rd = sub(rd, muls(n, 2.0f * dot(n, rd)));
                         ro = add(h.pos, muls(n, ETA));
-                        rtmin = ETA;
-                        rtmax = 5000.0f;
                         emit = true;
                         if (bounce + 1u < 50u) {
                             bounce++;
+                            inv = trav_inv<TRAV>(rd);
+                            trav_start<TRAV>(tr, stk, ETA, 5000.0f);
+                            tracing = true;
                             cnt.v[C_BOUNCE]++;
                         } else {
                             sample_done = true;
@@ -537,20 +676,20 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
                     }
                 } else {
                     // miss: background (w7e3) / environment_map(dir) * factor (w9e1.wgsl:264-265)
-                    res = add(res, W9 ? mul(V(L.env[0], L.env[1], L.env[2]), fac) : V(0, 0, 0));
+                    res = add(res, W9 ? mul(env, fac) : V(0, 0, 0));
                     sample_done = true;
                 }
-            } else {   // PH_SHADOW finished: rest of lambertian
-                res = add(res, add(hit ? zf : dvf, amb));
+            } else {
+                // shadow ray finished: rest of lambertian, then the bounce
+                res = add(res, tr.found ? cb : cu);
                 if (survive && bounce + 1u < 50u) {
-                    rd = indirect_dir(hnrm, rng);
-                    ro = hpos;
-                    rtmin = ETA;
-                    rtmax = 5000.0f;
+                    rd = ndir;   // origin = hit position, already in ro
+                    inv = trav_inv<TRAV>(rd);
+                    trav_start<TRAV>(tr, stk, ETA, 5000.0f);
                     emit = false;
-                    fac = divs(fac, prob);
                     bounce++;
-                    phase = PH_CLOSEST;
+                    shadow = false;
+                    tracing = true;
                     cnt.v[C_BOUNCE]++;
                 } else {
                     sample_done = true;
@@ -564,14 +703,49 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
                 a2 = rt_max0f((res.z + a2 * fi) / fi1);
                 it++;
                 if (it < it_end) {
-                    phase = PH_NEW;
+                    start_sample();
                 } else {
-                    L.accum[px.out] = make_float4(a0, a1, a2, 1.0f);
-                    if (L.ids) L.ids[px.out] = prim;
+                    L.accum[out] = make_float4(a0, a1, a2, 1.0f);
+                    if (L.ids) L.ids[out] = prim;
                     alive = false;
                 }
             }
         }
+        // ---- refill idle lanes with new pixels (ballot + mbcnt compaction)
+        for (;;) {
+            const uint64_t need = __ballot(!alive && !exhausted);
+            if (need == 0) break;
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(L.work_counter, (uint32_t)__popcll(need));
+            base = __shfl(base, (int)leader, 64);
+            if (!alive && !exhausted) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint32_t slot = base + rank;
+                if (slot >= nslots) {
+                    exhausted = true;
+                } else {
+                    const Pix p = map_pixel(L, slot >> 6, slot & 63u);
+                    if (p.valid) {
+                        px = p.x;
+                        py = p.y;
+                        out = p.out;
+                        it = L.first_iter;
+                        a0 = a1 = a2 = 0.0f;
+                        if (L.first_iter > 0u) {
+                            const float4 pa = L.accum[out];
+                            a0 = pa.x;
+                            a1 = pa.y;
+                            a2 = pa.z;
+                        }
+                        alive = true;
+                        start_sample();
+                    }
+                }
+            }
+        }
+        if (__ballot(alive) == 0) break;
     }
     flush_counters(cnt, L.counters, COUNT);
 }
@@ -607,7 +781,7 @@ __global__ void __launch_bounds__(256) k_primary(DevScene S, DevLaunch L, int pr
                                         : (void*)(lds_stack + threadIdx.x);
     const float ETA = 0.00001f;
     const uint32_t lane = threadIdx.x & 63u;
-    const Cam cam = make_cam(L.u);
+    const Cam cam = make_cam(L);
     const uint32_t subdiv = L.u.subdivision_level;
     const uint32_t nsamp = subdiv * subdiv;
     const uint32_t sel = L.u.selection1;
@@ -766,7 +940,7 @@ __device__ __forceinline__ bool w1_plane(f3 o, f3 w, float tmin, float& tmax, f3
 __global__ void __launch_bounds__(256) k_w1e6(DevLaunch L)
 {
     const uint32_t lane = threadIdx.x & 63u;
-    const Cam cam = make_cam(L.u);
+    const Cam cam = make_cam(L);
     Counters cnt;
 #pragma unroll
     for (int i = 0; i < C_N; i++) cnt.v[i] = 0;
@@ -853,7 +1027,7 @@ __host__ __device__ inline void math_eval(float x, float* o)
     o[3] = rt_det_cosf(x * 6.2831855f);
     o[4] = rt_det_acosf(x - __builtin_floorf(x));
     o[5] = (x * 3.0f + 1.0f) / (x - 7.0f);
-    o[6] = (float)(uint32_t)(x * 1000.0f) / (float)0x80000000u;
+    o[6] = (float)(uint32_t)((x < 0.0f ? -x : x) * 1000.0f) / (float)0x80000000u;
     o[7] = rt_det_acosf(rt_det_sqrtf(1.0f - (x - __builtin_floorf(x))));
 }
 __global__ void k_selftest_math(const float* in, float* out, uint32_t n)
@@ -861,6 +1035,31 @@ __global__ void k_selftest_math(const float* in, float* out, uint32_t n)
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) math_eval(in[i], out + (size_t)i * kMathOuts);
 }
+void camera_basis(const rt_uniform& u, float cam[14])
+{
+    auto nrm = [](float& x, float& y, float& z) {
+        const float l = rt_det_sqrtf(x * x + y * y + z * z);
+        x = x / l;
+        y = y / l;
+        z = z / l;
+    };
+    const float* e = u.camera_pos;
+    float v[3] = {u.camera_look_at[0] - e[0], u.camera_look_at[1] - e[1], u.camera_look_at[2] - e[2]};
+    nrm(v[0], v[1], v[2]);
+    const float* up = u.camera_up;
+    float b1[3] = {v[1] * up[2] - v[2] * up[1], v[2] * up[0] - v[0] * up[2], v[0] * up[1] - v[1] * up[0]};
+    nrm(b1[0], b1[1], b1[2]);
+    const float b2[3] = {b1[1] * v[2] - b1[2] * v[1], b1[2] * v[0] - b1[0] * v[2], b1[0] * v[1] - b1[1] * v[0]};
+    for (int i = 0; i < 3; i++) {
+        cam[i] = e[i];
+        cam[3 + i] = v[i];
+        cam[6 + i] = b1[i];
+        cam[9 + i] = b2[i];
+    }
+    cam[12] = u.camera_constant;
+    cam[13] = u.aspect_ratio;
+}
+
 void host_math(const float* in, float* out, uint32_t n)
 {
     for (uint32_t i = 0; i < n; i++) math_eval(in[i], out + (size_t)i * kMathOuts);

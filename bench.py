@@ -1,0 +1,232 @@
+"""Benchmark: Mrays/s (primary + shadow) of the BSP traversal + shading hot
+path at 1920x1080, 256 spp (BASELINE.json configs[2]: ~70k-tri bunny, W9E1
+path tracer), on N GPUs of one node.
+
+One step = one complete 1920x1080 x 256-spp progressive frame (iterations
+0..255, the reference's 256 RenderState::render() calls fused into one launch
+per GPU) with the framebuffer tiled across ranks (interleaved 8x8 tiles) and
+the finished tiles all-gathered over RCCL to assemble the frame on rank 0.
+Total work is fixed as N grows ("strong" scaling).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement".
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+METRIC = "Mrays/sec primary+shadow at 1920x1080; achieved HBM GB/s vs peak"
+
+
+def algorithmic_bytes(c, trav, npix, first_iter):
+    """reference-layout useful bytes of the traversal work,
+    plus the framebuffer bytes one launch moves (accum write, id write, accum
+    read when continuing)."""
+    if trav == "BSP":
+        t = 20 * c["node_interior"] + 16 * c["node_leaf"]
+    else:
+        t = 32 * c["bvh_pops"]
+    t += 4 * c["ids_read"] + 52 * c["tri_tests"] + 36 * c["tri_accepts"]
+    fb = npix * (16 + 4 + (16 if first_iter > 0 else 0))
+    return t + fb
+
+
+def cpu_baseline(args, mesh, cam, W, H, budget_s):
+    """The CPU oracle (a restatement of the reference WGSL path; the reference
+    itself needs Rust + Vulkan, absent here) on the host cores, over a bounded
+    sample of the same workload: a centred full-width band of rows, 1 spp per
+    pass, passes repeated until ~budget_s of CPU time."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_ffi as O
+    V, N, I, M, L = mesh.arrays()
+    om = O.OracleMesh(V, N, I, M, L)
+    osc = O.SceneRef(om, O.build_bsp(om) if args.trav == "BSP" else None,
+                     O.build_bvh(om) if args.trav == "BVH" else None, env=(1.0, 1.0, 1.0))
+    u = O.make_uniform(*cam, W, H)
+    cores = min(16, os.cpu_count() or 1)
+    rows = 64
+    region = (0, (H - rows) // 2, W, rows)
+    acc = None
+    rays = 0
+    it = 0
+    t0 = time.perf_counter()
+    while True:
+        acc, _, c = O.render(osc, u, "W9E1", args.trav, region, it, 1, accum=acc, nthreads=cores)
+        rays += c["primary"] + c["shadow"]
+        it += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or it >= 256:
+            break
+    return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"CPU oracle (C restatement of w9e1.wgsl+bsp.wgsl), {W}x{rows} centre band of the same "
+                      f"{W}x{H} frame, {it} spp, {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=256)
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--trav", default="BSP", choices=["BSP", "BVH"])
+    ap.add_argument("--ntris", type=int, default=69451)
+    ap.add_argument("--cpu-budget", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shade-threshold", type=int, default=None)
+    ap.add_argument("--waves-per-cu", type=int, default=None)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    # a real (non-null) stream shared by our kernels, torch's events and RCCL
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+
+    rt = importlib.import_module("02562_raytracer_amd")   # after torch: shares its HIP runtime
+    W, H = args.width, args.height
+    cam = ((-0.02, 0.11, 0.6), (-0.02, 0.11, 0.0), (0.0, 1.0, 0.0), 3.5)   # scenes.rs:71-77
+
+    t0 = time.perf_counter()
+    mesh = rt.Mesh.synth_bunny(args.ntris)
+    ctx = rt.Context(local)
+    ctx.set_stream(stream.cuda_stream)
+    if args.shade_threshold is not None:
+        ctx.set_option(rt._ffi.RT_OPT_SHADE_THRESHOLD, args.shade_threshold)
+    if args.waves_per_cu is not None:
+        ctx.set_option(rt._ffi.RT_OPT_WAVES_PER_CU, args.waves_per_cu)
+    ctx.upload_mesh(mesh)
+    if args.trav == "BSP":
+        accel = mesh.bsp_tree()
+        ctx.upload_bsp(accel)
+    else:
+        accel = mesh.bvh()
+        ctx.upload_bvh(accel)
+    ctx.set_environment((1.0, 1.0, 1.0))
+    ctx.set_uniforms(rt.make_uniform(*cam, W, H, selection1=0))
+    setup_s = time.perf_counter() - t0
+
+    lt = rt.local_tiles(W, H, world)
+    acc_local = torch.empty((lt * 64, 4), dtype=torch.float32, device=dev)
+    ids_local = torch.empty((lt * 64,), dtype=torch.int32, device=dev)
+    if world > 1:
+        acc_all = torch.empty((world * lt * 64, 4), dtype=torch.float32, device=dev)
+        ids_all = torch.empty((world * lt * 64,), dtype=torch.int32, device=dev)
+    frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
+    frame_ids = torch.empty((H, W), dtype=torch.int32, device=dev)
+
+    def step(events=None):
+        if events is not None:
+            events[0].record(stream)
+        ctx.render_tiles("W9E1", args.trav, rank, world, 0, args.spp, acc_local.data_ptr(), ids_local.data_ptr())
+        if events is not None:
+            events[1].record(stream)
+        if world > 1:
+            dist.all_gather_into_tensor(acc_all, acc_local)
+            dist.all_gather_into_tensor(ids_all, ids_local)
+            if rank == 0:
+                ctx.unpack_tiles(W, H, world, acc_all.data_ptr(), ids_all.data_ptr(), frame.data_ptr(),
+                                 frame_ids.data_ptr())
+        else:
+            ctx.unpack_tiles(W, H, 1, acc_local.data_ptr(), ids_local.data_ptr(), frame.data_ptr(),
+                             frame_ids.data_ptr())
+
+    # counted step (also the first warm-up): rays per step, deterministic
+    step()
+    counts = ctx.last_counts()
+    # counting instantiation: traversal counters for the algorithmic bytes
+    ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 1)
+    step()
+    detail = ctx.last_counts()
+    ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
+    for _ in range(max(0, args.warmup - 1)):
+        step()
+
+    rays = torch.tensor([counts["primary"] + counts["shadow"], counts["primary"], counts["shadow"],
+                         counts["bounce"], algorithmic_bytes(detail, args.trav, lt * 64, 0)],
+                        dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(rays)
+    rays = rays.cpu().numpy()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_ms = [float(x) for x in t.cpu().numpy()]
+
+    value = rays[0] * args.steps / elapsed / 1e6
+    if rank == 0:
+        # roofline of the dominant kernel (k_path W9E1 BSP): bytes of one launch
+        # on one GPU / its average HIP-event duration
+        bytes_per_launch = rays[4] / world
+        achieved = bytes_per_launch / (kern_ms / 1e3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                p = json.load(f)
+            key = f"{W}x{H}x{args.spp}_{args.trav}_n{world}"
+            traffic = p.get(key)
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args, mesh, cam, W, H, args.cpu_budget)
+        line = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "config": {"workload": f"bunny stand-in ({mesh.ntris} tris) W9E1 path trace, {args.trav} D20/leaf4, "
+                                   f"{W}x{H}, {args.spp} spp/step", "resolution": [W, H], "spp": args.spp,
+                       "traversal": args.trav, "ntris": mesh.ntris, "parallelism": f"tiles8x8/{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_path<W9E1,BSP>", "kernel_ms": round(kern_ms, 3),
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+            "cpu_baseline": cpu,
+            "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},
+            "traversal_per_launch": {k: detail[k] for k in ("node_interior", "node_leaf", "bvh_pops", "tri_tests",
+                                                            "tri_accepts", "trips", "lane_steps", "leaf_iters")},
+            "simd_lane_util": round(detail["lane_steps"] / max(1, 64 * detail["trips"]), 4),
+            "setup_s": round(setup_s, 3),
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

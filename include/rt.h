@@ -130,11 +130,17 @@ typedef struct rt_ray_counts {
     uint64_t ids_read;       /* treeIds / bvh_triangles reads              */
     uint64_t tri_tests;      /* ray-triangle tests                         */
     uint64_t tri_accepts;    /* accepted (closer) hits                     */
+    /* SIMD-efficiency diagnostics (detail instantiation only), per wave trip
+     * of the traversal loop: */
+    uint64_t trips;          /* traversal loop trips (sum over waves)      */
+    uint64_t lane_steps;     /* lanes that advanced a ray in those trips    */
+    uint64_t leaf_iters;     /* leaf-loop iterations executed (wave level) */
 } rt_ray_counts;
 
 /* ---- options (rt_set_option) ------------------------------------------- */
 #define RT_OPT_DETAIL_COUNTERS 1  /* 0/1: use the counting kernel instantiation    */
 #define RT_OPT_WAVES_PER_CU    2  /* persistent grid size: waves per CU (default 16) */
+#define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace; 64 = all lanes finish their rays first (lockstep) */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
 
