@@ -49,7 +49,7 @@ struct DevLaunch {
     float4* accum;
     uint32_t* ids;
     uint32_t* work_counter;       // zeroed before launch
-    unsigned long long* counters; // 10 x u64, zeroed before launch (rt_ray_counts order)
+    unsigned long long* counters; // 13 x u64, zeroed before launch (rt_ray_counts order)
 };
 
 // Launch the kernel for (mode, trav); detail = counting instantiation.

@@ -2,15 +2,17 @@
 // hot path of cakarsubasi/02562_raytracer (res/shaders/*.wgsl).
 //
 // Structure (DESIGN.md "Kernels"):
-//   * persistent grid: every wave dequeues 8x8-pixel tiles from a global atomic
-//     counter (one returning atomic per tile), so load balance does not depend
-//     on launch order and one wave = one coherent screen tile;
+//   * persistent grid (num_CUs x waves_per_CU waves): pixel slots come from a
+//     global atomic queue in 8x8-tile order, one atomic per wave refill, slots
+//     handed to the idle lanes with ballot + mbcnt (active-lane compaction);
 //   * one lane = one pixel, running all `spp` progressive iterations of that
 //     pixel in order (accumulation is sequential per pixel, w7e3.wgsl:261-271);
-//   * "while-while" ray state machine with ONE traversal call site: each step
-//     every live lane traces its current ray (camera / bounce closest-hit, or a
-//     shadow any-hit) through the same BSP/BVH loop, then advances its path;
-//     lanes never wait on a different ray type's code path;
+//   * ray state machine with ONE traversal call site: each loop trip every
+//     tracing lane advances its current ray (camera / bounce closest-hit, or a
+//     shadow any-hit) by at most one node and one triangle ("if-if"); lanes
+//     whose ray ended shade and start their next ray once few enough lanes
+//     are still tracing (shade_threshold), so no lane idles behind the
+//     slowest ray of its wave;
 //   * per-lane traversal stack in LDS (BSP: 8 B {far node, t} x MAX_LEVEL;
 //     BVH: 4 B x 50), [level][thread] layout => conflict-free ds_read/write_b64;
 //   * BSP nodes packed to 8 B (children implicit), triangles pre-transformed to

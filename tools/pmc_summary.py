@@ -1,14 +1,25 @@
 """Summarise rocprofv3 --pmc CSVs: per kernel, the mean per dispatch of every
-counter (summed over the counter's dimensions).  usage: pmc_summary.py <dir> [kernel-substring]"""
+counter (summed over the counter's dimensions), plus derived figures.
+
+  pmc_summary.py <dir> [kernel-substring] [--out FILE] [--traffic KEY]
+
+--traffic KEY records the kernel's HBM bytes per launch in
+profiles/pmc_traffic.json under KEY (bench.py reads it for roofline.traffic).
+HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB units): MI355X_MICROARCH.md
+"HBM / rocprofv3": on gfx950 FETCH_SIZE reports half the bytes of wide reads.
+"""
+import argparse
 import csv
 import glob
 import json
-import sys
+import os
 from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(root, ksub=None):
-    per = defaultdict(lambda: defaultdict(float))   # (kernel) -> counter -> sum over dispatches
+    per = defaultdict(lambda: defaultdict(float))   # kernel -> counter -> sum over dispatches
     disp = defaultdict(set)
     for f in sorted(glob.glob(f"{root}/**/*counter_collection.csv", recursive=True)):
         with open(f) as fh:
@@ -16,15 +27,49 @@ def load(root, ksub=None):
                 k = r["Kernel_Name"]
                 if ksub and ksub not in k:
                     continue
-                did = (f, r["Dispatch_Id"])
                 per[k][r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[(k, r["Counter_Name"])].add(did)
-    out = {}
-    for k, cs in per.items():
-        out[k] = {c: v / max(1, len(disp[(k, c)])) for c, v in cs.items()}
-    return out
+                disp[(k, r["Counter_Name"])].add((f, r["Dispatch_Id"]))
+    return {k: {c: v / max(1, len(disp[(k, c)])) for c, v in cs.items()} for k, cs in per.items()}
+
+
+def derived(c):
+    d = {}
+    if "FETCH_SIZE" in c and "WRITE_SIZE" in c:
+        d["hbm_bytes_per_launch"] = (2.0 * c["FETCH_SIZE"] + c["WRITE_SIZE"]) * 1024.0
+    if "TCC_HIT_sum" in c and "TCC_MISS_sum" in c:
+        d["l2_hit_rate"] = c["TCC_HIT_sum"] / max(1.0, c["TCC_HIT_sum"] + c["TCC_MISS_sum"])
+    if "TCP_TCC_READ_REQ_sum" in c and "TCP_TOTAL_CACHE_ACCESSES_sum" in c:
+        d["l1_hit_rate"] = 1.0 - c["TCP_TCC_READ_REQ_sum"] / max(1.0, c["TCP_TOTAL_CACHE_ACCESSES_sum"])
+    if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c:
+        d["valu_lane_util"] = c["SQ_THREAD_CYCLES_VALU"] / max(1.0, 64.0 * c["SQ_ACTIVE_INST_VALU"])
+    if "SQ_INSTS_VALU" in c and "SQ_INSTS_SALU" in c:
+        d["salu_per_valu"] = c["SQ_INSTS_SALU"] / max(1.0, c["SQ_INSTS_VALU"])
+    if "SQ_WAIT_ANY" in c and "SQ_WAVE_CYCLES" in c:
+        d["wait_frac"] = c["SQ_WAIT_ANY"] / max(1.0, c["SQ_WAVE_CYCLES"])
+    return d
 
 
 if __name__ == "__main__":
-    res = load(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else None)
-    print(json.dumps(res, indent=1))
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("kernel", nargs="?")
+    ap.add_argument("--out")
+    ap.add_argument("--traffic")
+    a = ap.parse_args()
+    res = load(a.dir, a.kernel)
+    out = {k: {"counters": c, "derived": derived(c)} for k, c in res.items()}
+    txt = json.dumps(out, indent=1)
+    print(txt)
+    if a.out:
+        with open(a.out, "w") as f:
+            f.write(txt + "\n")
+    if a.traffic:
+        if len(res) != 1:
+            raise SystemExit(f"--traffic needs exactly one kernel, got {list(res)}")
+        (c,) = res.values()
+        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        cur = json.load(open(path)) if os.path.exists(path) else {}
+        cur[a.traffic] = int(derived(c)["hbm_bytes_per_launch"])
+        with open(path, "w") as f:
+            json.dump(cur, f, indent=1, sort_keys=True)
+            f.write("\n")
