@@ -62,7 +62,8 @@ class Tileset(C.Structure):
 
 
 COUNT_FIELDS = ["samples", "primary", "shadow", "bounce", "node_interior", "node_leaf", "bvh_pops",
-                "ids_read", "tri_tests", "tri_accepts", "trips", "lane_steps", "leaf_iters"]
+                "ids_read", "tri_tests", "tri_accepts", "trips", "lane_steps", "leaf_iters", "shade_passes",
+                "shade_lanes", "trav_cycles", "shade_cycles"]
 
 
 class RayCounts(C.Structure):

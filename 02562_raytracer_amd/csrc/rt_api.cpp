@@ -63,7 +63,8 @@ struct rt_ctx {
     uint32_t nverts = 0, ntris = 0, nmats = 0, nlights = 0;
     bool has_mesh = false;
     DevBuf pos, nrm, idx, mats, lights;
-    DevBuf bsp_nodes, bsp_recs, bsp_ids;
+    DevBuf bsp_nodes, bsp_ids;   // bsp_nodes: [8-B nodes | 48-B records]
+    uint32_t bsp_rec_off = 0;
     uint32_t bsp_depth = 0;
     float aabb[6] = {0, 0, 0, 0, 0, 0};
     bool has_bsp = false;
@@ -186,7 +187,7 @@ int rt_create(int device, rt_ctx** out)
     memset(&c->u, 0, sizeof c->u);
     memset(&c->last, 0, sizeof c->last);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
-        c->work.alloc(64) != hipSuccess || c->counters.alloc(16 * sizeof(unsigned long long)) != hipSuccess) {
+        c->work.alloc(64) != hipSuccess || c->counters.alloc(32 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return fail(nullptr, RT_E_DEVICE, "rt_create: stream/buffer setup failed");
     }
@@ -368,12 +369,14 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
         if (ids[k] >= c->ntris) return fail(c, RT_E_INVALID, "rt_upload_bsp: triangle id out of range");
     // validate the reachable tree (implicit children, leaves inside ids)
     std::vector<uint32_t> stack{0};
-    std::vector<uint32_t> packed((size_t)nnodes * 2, 0u);
+    // 8-B device nodes, 1-based heap order: slot 0 is padding, node i at slot i+1
+    // (the kernel walks 1-based indices; sibling pairs 2M, 2M+1 share 16 B)
+    std::vector<uint32_t> packed(((size_t)nnodes + 1) * 2, 0u);
     for (uint32_t i = 0; i < nnodes; i++) {
-        packed[2 * (size_t)i] = tree[4 * (size_t)i];
+        packed[2 * ((size_t)i + 1)] = tree[4 * (size_t)i];
         uint32_t pbits;
         memcpy(&pbits, &planes[i], 4);
-        packed[2 * (size_t)i + 1] = (tree[4 * (size_t)i] & 3u) == 3u ? tree[4 * (size_t)i + 1] : pbits;
+        packed[2 * ((size_t)i + 1) + 1] = (tree[4 * (size_t)i] & 3u) == 3u ? tree[4 * (size_t)i + 1] : pbits;
     }
     while (!stack.empty()) {
         const uint32_t i = stack.back();
@@ -396,8 +399,20 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_bsp = false;
     int r;
-    if ((r = upload(c, c->bsp_nodes, packed.data(), packed.size() * 4))) return r;
-    if ((r = upload(c, c->bsp_recs, recs.data(), recs.size() * 4))) return r;
+    // one allocation [nodes | records]: the kernel reads both through one buffer
+    // resource with 32-bit offsets (node treelets and triangle records are
+    // fetched by the same loads, DESIGN.md "Data layout in HBM")
+    const size_t node_bytes = (packed.size() * 4 + 255) & ~(size_t)255;
+    const size_t total = node_bytes + recs.size() * 4;
+    if (total >= ((size_t)1 << 32) || (size_t)nnodes * 32 + 64 >= ((size_t)1 << 32))
+        return fail(c, RT_E_UNSUPPORTED, "rt_upload_bsp: BSP nodes + records must stay below 4 GiB (max_depth <= 26)");
+    {
+        std::vector<uint8_t> blob(total, 0);
+        memcpy(blob.data(), packed.data(), packed.size() * 4);
+        memcpy(blob.data() + node_bytes, recs.data(), recs.size() * 4);
+        if ((r = upload(c, c->bsp_nodes, blob.data(), blob.size()))) return r;
+    }
+    c->bsp_rec_off = (uint32_t)node_bytes;
     if ((r = upload(c, c->bsp_ids, ids, (size_t)nids * 4))) return r;
     c->bsp_depth = max_depth;
     c->aabb[0] = aabb[0];
@@ -507,7 +522,9 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     S.nmats = c->nmats;
     S.nlights = c->nlights;
     S.bsp_nodes = c->bsp_nodes.as<uint2>();
-    S.bsp_recs = c->bsp_recs.as<float4>();
+    S.bsp_recs = reinterpret_cast<const float4*>(c->bsp_nodes.as<uint8_t>() + c->bsp_rec_off);
+    S.bsp_bytes = (uint32_t)c->bsp_nodes.n;
+    S.bsp_rec_off = c->bsp_rec_off;
     S.bsp_ids = c->bsp_ids.as<uint32_t>();
     S.bsp_depth = c->bsp_depth;
     memcpy(S.aabb, c->aabb, sizeof S.aabb);
@@ -523,7 +540,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     L.shade_threshold = (uint32_t)c->shade_threshold;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->work.p, 0, 64, c->stream));
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 16 * sizeof(unsigned long long), c->stream));
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
     if (L.nwork == 0) return RT_OK;
     int r = rtk::launch_render(S, L, mode, trav, c->detail, c->num_cus, c->waves_per_cu, c->stream);
     if (r) return fail(c, r, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
@@ -607,7 +624,8 @@ int rt_last_counts(rt_ctx* c, rt_ray_counts* counts)
 {
     if (!c || !counts) return RT_E_INVALID;
     if (int r = set_dev(c)) return r;
-    unsigned long long h[16];
+    unsigned long long h[32];
+    static_assert(sizeof(rt_ray_counts) <= sizeof h, "counter buffer");
     HIPCHK(c, hipMemcpyAsync(h, c->counters.p, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     uint64_t* dst = reinterpret_cast<uint64_t*>(counts);

@@ -17,10 +17,12 @@ struct DevScene {
     const rt_material* mats;
     const uint32_t* lights;
     uint32_t nverts, ntris, nmats, nlights;
-    // BSP: 8-byte nodes {x = axis|count<<2, y = plane bits (interior) / first id (leaf)};
+    // BSP: 8-byte nodes {x = axis|count<<2, y = plane bits (interior) / first id (leaf)}, 1-based (slot 0 pad);
     // children implicit (2i+1, 2i+2, src/data_structures/bsp_tree.rs:137-140).
-    const uint2* bsp_nodes;
+    const uint2* bsp_nodes;       // start of one allocation [nodes | records]
     const float4* bsp_recs;       // 3 x float4 per treeIds slot: v0, e0=v1-v0, e1=v2-v0, n=cross(e0,e1)
+    uint32_t bsp_bytes;           // size of the allocation (buffer-resource range)
+    uint32_t bsp_rec_off;         // byte offset of the records
     const uint32_t* bsp_ids;      // treeIds
     uint32_t bsp_depth;           // MAX_LEVEL
     float aabb[6];                // root BboxGpu min.xyz, max.xyz
@@ -49,7 +51,7 @@ struct DevLaunch {
     float4* accum;
     uint32_t* ids;
     uint32_t* work_counter;       // zeroed before launch
-    unsigned long long* counters; // 13 x u64, zeroed before launch (rt_ray_counts order)
+    unsigned long long* counters; // 32 x u64, zeroed before launch (rt_ray_counts order)
 };
 
 // Launch the kernel for (mode, trav); detail = counting instantiation.

@@ -13,8 +13,9 @@
 //     whose ray ended shade and start their next ray once few enough lanes
 //     are still tracing (shade_threshold), so no lane idles behind the
 //     slowest ray of its wave;
-//   * per-lane traversal stack in LDS (BSP: 8 B {far node, t} x MAX_LEVEL;
-//     BVH: 4 B x 50), [level][thread] layout => conflict-free ds_read/write_b64;
+//   * per-lane traversal stack in LDS, [level][thread] layout (conflict-free):
+//     BSP: a bit trail in a register + 4-B t per depth (MAX_LEVEL entries);
+//     BVH: 4-B node indices x 50;
 //   * BSP nodes packed to 8 B (children implicit), triangles pre-transformed to
 //     48-B records {v0, e0, e1, n} in treeIds order (one 3 x dwordx4 gather).
 // Numerics: -ffp-contract=off, correctly rounded f32 div/sqrt, pinned
@@ -72,7 +73,7 @@ __device__ __forceinline__ float rnd(uint32_t& prev) { return (float)mcg31(prev)
 
 // ------------------------------------------------------------------ counters
 enum { C_SAMPLES, C_PRIMARY, C_SHADOW, C_BOUNCE, C_INTERIOR, C_LEAF, C_POPS, C_IDS, C_TESTS, C_ACCEPTS,
-       C_TRIPS, C_LANE_STEPS, C_LEAF_ITERS, C_N };
+       C_TRIPS, C_LANE_STEPS, C_LEAF_ITERS, C_SHADE_PASSES, C_SHADE_LANES, C_TRAV_CYC64, C_SHADE_CYC64, C_N };
 
 struct Counters {
     uint32_t v[C_N];
@@ -85,6 +86,7 @@ __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long 
     for (int i = 0; i < n; i++) {
         uint32_t x = c.v[i];
         unsigned long long s = x;
+        if (i == C_TRAV_CYC64 || i == C_SHADE_CYC64) s <<= 6;   // wave cycles, accumulated in units of 64
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
         if ((threadIdx.x & 63u) == 0 && s) atomicAdd(out + i, s);
@@ -173,29 +175,38 @@ __device__ __forceinline__ bool sign_certain_neg(float a, float den)
 __device__ __forceinline__ bool sign_uncertain(float a) { return a != 0.0f && !(rt_absf(a) >= 0x1p-60f); }
 
 template <bool FAST>
-__device__ __forceinline__ bool tri_test(const float4* recs, uint32_t k, f3 o, f3 w, float tmin, float tmax,
-                                         float& dist, float& beta, float& gamma)
+__device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const float4 r2, f3 o, f3 w, float tmin,
+                                         float tmax, float& dist, float& beta, float& gamma)
 {
-    const float4 r0 = recs[3u * k], r1 = recs[3u * k + 1u], r2 = recs[3u * k + 2u];
     const f3 v0 = V(r0.x, r0.y, r0.z), e0 = V(r0.w, r1.x, r1.y), e1 = V(r1.z, r1.w, r2.x);
     const f3 n = V(r2.y, r2.z, r2.w);
     const f3 ov = sub(v0, o);
     const f3 nom = cross(ov, w);
     const float denom = dot(w, n);
-    if (rt_absf(denom) < 1e-10f) return false;
     const float a = dot(nom, e1);
     const float b = -dot(nom, e0);
     const float c = dot(ov, n);
-    if (FAST && rt_absf(denom) <= 0x1p60f) {
-        if (sign_certain_neg(a, denom) || sign_certain_neg(b, denom)) return false;
+    bool reject = rt_absf(denom) < 1e-10f;
+    if (FAST) {
         const float tq = c * __builtin_amdgcn_rcpf(denom);
         const float m = rt_absf(tq) * 0x1p-20f + 1e-30f;
-        if (tq - m > tmax || tq + m < tmin) return false;
+        reject = reject || (rt_absf(denom) <= 0x1p60f && (sign_certain_neg(a, denom) || sign_certain_neg(b, denom) ||
+                                                         tq - m > tmax || tq + m < tmin));
     }
+    if (reject) return false;
     beta = a / denom;
     gamma = b / denom;
     dist = c / denom;
     return !(beta < 0.0f || gamma < 0.0f || beta + gamma > 1.0f || dist > tmax || dist < tmin);
+}
+template <bool FAST>
+__device__ __forceinline__ bool tri_test(const float4* recs, uint32_t k, f3 o, f3 w, float tmin, float tmax,
+                                         float& dist, float& beta, float& gamma)
+{
+    // all three 16-B pieces are loaded before the first decision, so a test
+    // costs one memory round trip (an early |denom| exit would let the
+    // compiler sink the r0/r1 loads behind the r2 load)
+    return tri_math<FAST>(recs[3u * k], recs[3u * k + 1u], recs[3u * k + 2u], o, w, tmin, tmax, dist, beta, gamma);
 }
 
 struct TraceOut {
@@ -204,18 +215,21 @@ struct TraceOut {
 };
 
 // Per-lane traversal state (kept in registers across the persistent loop).
+// The accepted hit's distance is tmax (every accept sets tmax = dist, and
+// neither walk raises tmax again after its last accept).
 struct Trav {
-    uint32_t node;   // BSP: current node      BVH: stack top
-    uint32_t lvl;    // BSP: stack depth       BVH: pops so far
+    uint32_t node;   // BSP: 1-based heap index of the current node   BVH: stack top
+    uint32_t lvl;    // BSP: bit trail (bit d = pending far child pushed at depth d)   BVH: pops so far
     uint32_t leaf_k, leaf_end;   // triangle slots of the leaf being tested (empty when equal)
     float tmin, tmax, tmax0;
     bool found;
-    TraceOut best;
+    uint32_t hit_k;
+    float beta, gamma;
 };
 
 __device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
 {
-    t.node = 0;
+    t.node = 1;
     t.lvl = 0;
     t.leaf_k = t.leaf_end = 0;
     t.tmin = tmin;
@@ -223,6 +237,7 @@ __device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
     t.tmax0 = tmax;
     t.found = false;
 }
+__device__ __forceinline__ TraceOut trav_out(const Trav& t) { return TraceOut{t.hit_k, t.beta, t.gamma, t.tmax}; }
 
 // One triangle test of the current leaf (shared by BSP and BVH).
 template <bool COUNT>
@@ -237,10 +252,9 @@ __device__ __forceinline__ void leaf_test(const float4* recs, const f3 o, const 
         if (COUNT) c.v[C_ACCEPTS]++;
         t.tmax = dist;
         t.found = true;
-        t.best.k = t.leaf_k;
-        t.best.beta = beta;
-        t.best.gamma = gamma;
-        t.best.dist = dist;
+        t.hit_k = t.leaf_k;
+        t.beta = beta;
+        t.gamma = gamma;
     }
     t.leaf_k++;
 }
@@ -249,74 +263,155 @@ __device__ __forceinline__ void leaf_test(const float4* recs, const f3 o, const 
 // intersect_trimesh, bsp.wgsl:10-81, as a per-lane state machine: each call
 // visits at most one node and tests at most one triangle ("if-if"), so a wave
 // trip never serialises behind the longest leaf of any lane.  Returns true
-// when the ray is finished (t.found = hit).  The explicit stack keeps
-// {far node, t}; the tmax a pop restores is the t of the entry below it (or
-// the ray's original tmax): exactly the value bsp.wgsl saves in branch_ray.y
-// (tmax only changes on push, pop, and on an accept, after which the walk ends).
+// when the ray is finished (t.found = hit).
+//
+// Stack as a bit trail.  Nodes are numbered 1-based in heap order (children
+// 2M, 2M+1; the device array has one pad node in front, so node M is at
+// [M]).  Every pending stack entry of bsp.wgsl is an ancestor of the current
+// node at which the walk pushed its far child, so an entry is fully described
+// by its depth d: bit d of `lvl` marks it, the far child is the sibling of
+// the current node's ancestor at depth d+1, ((M >> (depth(M)-d-1)) ^ 1), and
+// only its t is stored -- in LDS, indexed by depth ([depth][thread], 4 B).
+// The tmax a pop restores is the t of the next pending entry below (or the
+// ray's original tmax): exactly the value bsp.wgsl saves in branch_ray.y,
+// since tmax only changes on push, pop, and on an accept, after which the
+// walk ends.
 // anyhit: stop at the first accepted triangle -- shadow rays use only the
 // boolean, and the walk up to that triangle is identical, so it is too.
 // Interior nodes: the exact t = RN((plane - o)/denom) is only divided out when
 // the approximate t (v_rcp_f32, 2^-20 margin) cannot decide near/far.
-__device__ __forceinline__ bool bsp_pop(uint2* stk, Trav& t)
+__device__ __forceinline__ uint32_t heap_depth(uint32_t m) { return 31u - (uint32_t)__clz((int)m); }
+
+__device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 {
     if (t.lvl == 0) return true;   // `branch_lvl == 0u` -> return false (miss)
-    t.lvl--;
-    const uint2 e = stk[t.lvl * 256u];
-    t.node = e.x;
-    t.tmin = __uint_as_float(e.y);
-    t.tmax = t.lvl ? __uint_as_float(stk[(t.lvl - 1u) * 256u].y) : t.tmax0;
+    const uint32_t d = heap_depth(t.lvl);
+    t.lvl ^= 1u << d;
+    t.node = (t.node >> (heap_depth(t.node) - d - 1u)) ^ 1u;
+    t.tmin = stk[d * 256u];
+    t.tmax = t.lvl ? stk[heap_depth(t.lvl) * 256u] : t.tmax0;
     return false;
 }
 
-template <bool COUNT>
-__device__ __forceinline__ bool bsp_step(const DevScene& S, uint2* stk, const f3 o, const f3 d, const f3 inv,
-                                         bool anyhit, Trav& t, Counters& c)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 as_f4(v4u q)
 {
-    if (t.leaf_k == t.leaf_end) {
-        const uint2 n = S.bsp_nodes[t.node];
-        const uint32_t axis = n.x & 3u;
-        if (axis == 3u) {
-            if (COUNT) c.v[C_LEAF]++;
-            const uint32_t count = n.x >> 2;
-            if (COUNT) c.leafc = count;
-            if (count == 0u) return bsp_pop(stk, t);
-            t.leaf_k = n.y;
-            t.leaf_end = n.y + count;
+    return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
+}
+
+// One interior-node decision of bsp.wgsl:54-78 at node m (data n).  Returns
+// the next node; pushes {depth(m), t} when both children are visited.
+template <bool COUNT>
+__device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, const f3 o, const f3 d,
+                                               const f3 inv, Trav& t, Counters& c)
+{
+    if (COUNT) c.v[C_INTERIOR]++;
+    const uint32_t axis = n.x & 3u;
+    const float ad = comp(d, axis), ao = comp(o, axis);
+    const uint32_t near_node = 2u * m + (ad >= 0.0f ? 0u : 1u);
+    const float x = __uint_as_float(n.y) - ao;
+    const float tq = x * comp(inv, axis);
+    const float mg = rt_absf(tq) * 0x1p-20f + 1e-30f;
+    uint32_t next = near_node;
+    if (!(tq - mg > t.tmax)) {   // not certainly t > tmax
+        if (tq + mg < t.tmin && tq + mg <= t.tmax) {   // certainly !(t > tmax) && t < tmin
+            next = near_node ^ 1u;
         } else {
-            if (COUNT) c.v[C_INTERIOR]++;
-            const float ad = comp(d, axis), ao = comp(o, axis);
-            const uint32_t left = 2u * t.node + 1u;
-            const uint32_t near_node = ad >= 0.0f ? left : left + 1u;
-            const uint32_t far_node = ad >= 0.0f ? left + 1u : left;
-            const float x = __uint_as_float(n.y) - ao;
-            const float tq = x * comp(inv, axis);
-            const float m = rt_absf(tq) * 0x1p-20f + 1e-30f;
-            if (tq - m > t.tmax) {   // certainly t > tmax
-                t.node = near_node;
-            } else if (tq + m < t.tmin && tq + m <= t.tmax) {   // certainly !(t > tmax) && t < tmin
-                t.node = far_node;
-            } else {
-                const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
-                const float tt = x / denom;
-                if (tt > t.tmax) {
-                    t.node = near_node;
-                } else if (tt < t.tmin) {
-                    t.node = far_node;
+            const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
+            const float tt = x / denom;
+            if (!(tt > t.tmax)) {
+                if (tt < t.tmin) {
+                    next = near_node ^ 1u;
                 } else {
-                    stk[t.lvl * 256u] = make_uint2(far_node, __float_as_uint(tt));
-                    t.lvl++;
+                    const uint32_t dep = heap_depth(m);
+                    stk[dep * 256u] = tt;
+                    t.lvl |= 1u << dep;
                     t.tmax = tt;
-                    t.node = near_node;
                 }
             }
-            return false;
         }
     }
-    leaf_test<COUNT>(S.bsp_recs, o, d, t, c);
-    if (t.found && anyhit) t.leaf_k = t.leaf_end;
-    if (t.leaf_k != t.leaf_end) return false;
-    if (t.found) return true;   // a leaf with an accepted triangle ends the walk
-    return bsp_pop(stk, t);
+    return next;
+}
+
+// Node reached by the walk: a leaf starts its triangle range (tested from the
+// next trip on) or, when empty, pops.  Returns true when the ray is finished.
+template <bool COUNT>
+__device__ __forceinline__ bool bsp_leaf(const float* stk, const uint2 n, Trav& t, Counters& c)
+{
+    if (COUNT) c.v[C_LEAF]++;
+    const uint32_t count = n.x >> 2;
+    if (COUNT) c.leafc = count;
+    t.leaf_k = n.y;
+    t.leaf_end = n.y + count;
+    return count == 0u ? bsp_pop(stk, t) : false;
+}
+
+// One trip of a lane through intersect_trimesh (bsp.wgsl:10-81).  Every trip
+// issues its loads together, before any decision (one memory round trip):
+//   * a lane inside a leaf tests one triangle: its 48-B record;
+//   * a lane walking nodes fetches the 3-level treelet below its node m:
+//     the 16 B holding node m, the sibling pair {2m, 2m+1} (16 B) and the
+//     grandchildren {4m..4m+3} (32 B) -- 1-based heap order keeps pairs and
+//     quads aligned -- and walks up to three levels with no further load.
+// Nodes and records share one buffer resource, so the four 16-B loads are the
+// same instructions for both kinds of lane (out-of-range offsets read 0).
+template <bool COUNT>
+__device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
+                                         bool anyhit, Trav& t, Counters& c)
+{
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
+    const bool in_leaf = t.leaf_k != t.leaf_end;
+    const uint32_t rec = S.bsp_rec_off + 48u * t.leaf_k;
+    const uint32_t m = t.node;
+    const uint32_t o0 = in_leaf ? rec : 8u * (m & ~1u);
+    const uint32_t o1 = in_leaf ? rec + 16u : 16u * m;
+    const uint32_t o2 = in_leaf ? rec + 32u : 32u * m;
+    const uint32_t o3 = in_leaf ? 0xFFFFFFF0u : 32u * m + 16u;
+    v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o0, 0, 0);
+    v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o1, 0, 0);
+    v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, o2, 0, 0);
+    v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, o3, 0, 0);
+    // keep the four loads together (the compiler would sink q3 into the
+    // level-2 branch: a second round trip)
+    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+    if (in_leaf) {
+        if (COUNT) {
+            c.v[C_IDS]++;
+            c.v[C_TESTS]++;
+        }
+        float dist, beta, gamma;
+        if (tri_math<true>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma)) {
+            if (COUNT) c.v[C_ACCEPTS]++;
+            t.tmax = dist;
+            t.found = true;
+            t.hit_k = t.leaf_k;
+            t.beta = beta;
+            t.gamma = gamma;
+            if (anyhit) return true;
+        }
+        t.leaf_k++;
+        if (t.leaf_k != t.leaf_end) return false;
+        if (t.found) return true;   // a leaf with an accepted triangle ends the walk
+        return bsp_pop(stk, t);
+    }
+    // level 0: node m
+    uint2 n = (m & 1u) ? make_uint2(q0.z, q0.w) : make_uint2(q0.x, q0.y);
+    if ((n.x & 3u) == 3u) return bsp_leaf<COUNT>(stk, n, t, c);
+    uint32_t nx = bsp_decide<COUNT>(stk, n, m, o, d, inv, t, c);
+    // level 1: a child of m, from the pair {2m, 2m+1}
+    n = (nx & 1u) ? make_uint2(q1.z, q1.w) : make_uint2(q1.x, q1.y);
+    t.node = nx;
+    if ((n.x & 3u) == 3u) return bsp_leaf<COUNT>(stk, n, t, c);
+    nx = bsp_decide<COUNT>(stk, n, t.node, o, d, inv, t, c);
+    // level 2: a grandchild of m, from the quad {4m .. 4m+3}
+    const v4u g = (nx & 2u) ? q3 : q2;
+    n = (nx & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
+    t.node = nx;
+    if ((n.x & 3u) == 3u) return bsp_leaf<COUNT>(stk, n, t, c);
+    t.node = bsp_decide<COUNT>(stk, n, t.node, o, d, inv, t, c);
+    return false;
 }
 
 // 1/denom per axis for the approximate interior-node test (denom as bsp.wgsl:63)
@@ -412,7 +507,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const f3
                                           bool anyhit, Trav& t, Counters& c)
 {
     if (TRAV == RT_TRAVERSE_BVH) return bvh_step<COUNT>(S, reinterpret_cast<uint32_t*>(stk), o, d, inv, anyhit, t, c);
-    return bsp_step<COUNT>(S, reinterpret_cast<uint2*>(stk), o, d, inv, anyhit, t, c);
+    return bsp_step<COUNT>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
 }
 
 // Whole traversal of one ray (used by the primary-ray kernel).
@@ -425,7 +520,7 @@ __device__ __forceinline__ bool trace(const DevScene& S, void* stk, const f3 o, 
     const f3 inv = trav_inv<TRAV>(d);
     for (uint32_t guard = 0; guard < (1u << 24); guard++)
         if (trav_step<TRAV, COUNT>(S, stk, o, d, inv, anyhit, t, c)) break;
-    out = t.best;
+    out = trav_out(t);
     return t.found;
 }
 
@@ -540,9 +635,8 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 template <int MODE, int TRAV, bool COUNT>
 __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
 {
-    extern __shared__ uint2 lds_stack[];
-    void* stk = TRAV == RT_TRAVERSE_BVH ? (void*)(reinterpret_cast<uint32_t*>(lds_stack) + threadIdx.x)
-                                        : (void*)(lds_stack + threadIdx.x);
+    extern __shared__ uint32_t lds_stack[];   // [level][thread], 4 B entries
+    void* stk = lds_stack + threadIdx.x;
     constexpr bool W9 = MODE == RT_MODE_W9E1;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
@@ -591,11 +685,14 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
         cnt.v[C_PRIMARY]++;
     };
 
+    uint64_t tstamp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
-        const uint64_t trm = __ballot(alive && tracing);
-        const uint64_t wtm = __ballot(alive && !tracing);
-        if (trm != 0 && (wtm == 0 || T >= 64u || (uint32_t)__popcll(trm) > T)) {
-            // ---- traversal phase: one node per tracing lane
+        // ---- traversal phase: every tracing lane advances its ray by one node
+        //      visit / triangle test per trip, until enough lanes wait to shade
+        for (;;) {
+            const uint64_t trm = __ballot(alive && tracing);
+            const uint64_t wtm = __ballot(alive && !tracing);
+            if (!(trm != 0 && (wtm == 0 || T >= 64u || (uint32_t)__popcll(trm) > T))) break;
             if (COUNT) cnt.leafc = 0;
             if (alive && tracing) {
                 if (COUNT) cnt.v[C_LANE_STEPS]++;
@@ -610,14 +707,22 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
                     cnt.v[C_LEAF_ITERS] += mx;
                 }
             }
-            continue;
+        }
+        if (COUNT) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            if (lane == 0) {
+                cnt.v[C_TRAV_CYC64] += (uint32_t)((now - tstamp) >> 6);
+                cnt.v[C_SHADE_PASSES]++;
+            }
+            if (alive && !tracing) cnt.v[C_SHADE_LANES]++;
+            tstamp = now;
         }
         // ---- shading phase
         if (alive && !tracing) {
             bool sample_done = false;
             if (!shadow) {
                 if (tr.found) {
-                    const HitRec h = resolve<TRAV>(S, tr.best, ro, rd, !W9);
+                    const HitRec h = resolve<TRAV>(S, trav_out(tr), ro, rd, !W9);
                     if (bounce == 0) prim = h.tri;
                     const rt_material& m = mat_of(S, h.material);
                     if (sel == 0u) {
@@ -747,6 +852,11 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
                 }
             }
         }
+        if (COUNT) {
+            const uint64_t now = __builtin_amdgcn_s_memtime();
+            if (lane == 0) cnt.v[C_SHADE_CYC64] += (uint32_t)((now - tstamp) >> 6);
+            tstamp = now;
+        }
         if (__ballot(alive) == 0) break;
     }
     flush_counters(cnt, L.counters, COUNT);
@@ -778,9 +888,8 @@ __device__ __forceinline__ bool intersect_min_max(const float* aabb, const f3 o,
 template <int TRAV, bool COUNT>
 __global__ void __launch_bounds__(256) k_primary(DevScene S, DevLaunch L, int project)
 {
-    extern __shared__ uint2 lds_stack[];
-    void* stk = TRAV == RT_TRAVERSE_BVH ? (void*)(reinterpret_cast<uint32_t*>(lds_stack) + threadIdx.x)
-                                        : (void*)(lds_stack + threadIdx.x);
+    extern __shared__ uint32_t lds_stack[];   // [level][thread], 4 B entries
+    void* stk = lds_stack + threadIdx.x;
     const float ETA = 0.00001f;
     const uint32_t lane = threadIdx.x & 63u;
     const Cam cam = make_cam(L);
@@ -1090,7 +1199,7 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
                   int waves_per_cu, hipStream_t stream)
 {
     const int grid = grid_for(num_cus, waves_per_cu);
-    const size_t lds = trav == RT_TRAVERSE_BVH ? (size_t)50 * 256 * 4 : (size_t)(s.bsp_depth ? s.bsp_depth : 1) * 256 * 8;
+    const size_t lds = trav == RT_TRAVERSE_BVH ? (size_t)50 * 256 * 4 : (size_t)(s.bsp_depth ? s.bsp_depth : 1) * 256 * 4;
     if (mode == RT_MODE_W1E6) {
         hipLaunchKernelGGL(k_w1e6, dim3(grid), dim3(256), 0, stream, l);
         return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;

@@ -135,6 +135,12 @@ typedef struct rt_ray_counts {
     uint64_t trips;          /* traversal loop trips (sum over waves)      */
     uint64_t lane_steps;     /* lanes that advanced a ray in those trips    */
     uint64_t leaf_iters;     /* leaf-loop iterations executed (wave level) */
+    /* path kernels, per wave: shading passes, lanes shaded, and wave cycles
+     * (s_memtime) spent in the traversal and in the shading/refill phases */
+    uint64_t shade_passes;
+    uint64_t shade_lanes;
+    uint64_t trav_cycles;
+    uint64_t shade_cycles;
 } rt_ray_counts;
 
 /* ---- options (rt_set_option) ------------------------------------------- */

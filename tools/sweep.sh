@@ -1,7 +1,10 @@
 #!/bin/bash
-# parameter sweep of the bench kernel (short runs); usage: tools/sweep.sh <out> <spp> "<opt sets>"
+# Parameter sweep of the bench kernel (short runs).
+# usage: tools/sweep.sh <out> <spp> "<bench opts 1>" "<bench opts 2>" ...
 OUT=$1; SPP=$2; shift 2
 for o in "$@"; do
   echo "== $o" >> $OUT
-  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 --spp $SPP $o 2>&1 | grep '^{' | python -c "import json,sys; d=json.loads(sys.stdin.read()); t=d['traversal_per_launch']; print(d['value'], d['ms_per_step'], d['roofline']['kernel_ms'], d['roofline']['frac'], 'util', d['simd_lane_util'], 'leaf_iters/trip', round(t['leaf_iters']/max(1,t['trips']),3))" >> $OUT || { echo FAIL >> $OUT; exit 1; }
+  timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 --warmup 1 --spp $SPP $o > $OUT.tmp 2>&1 || { cat $OUT.tmp >> $OUT; echo FAIL >> $OUT; exit 1; }
+  grep '^{' $OUT.tmp | python tools/bench_brief.py >> $OUT || { cat $OUT.tmp >> $OUT; exit 1; }
 done
+rm -f $OUT.tmp
