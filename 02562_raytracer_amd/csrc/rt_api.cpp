@@ -55,7 +55,7 @@ struct rt_ctx {
     std::string err;
     int num_cus = 256;
     int waves_per_cu = 16;
-    int shade_threshold = 16;
+    int shade_threshold = 32;
     bool detail = false;
     // host copies needed to build the triangle records on BSP/BVH upload
     std::vector<float> h_pos;

@@ -170,7 +170,7 @@ __device__ __forceinline__ void pixel_uv(const rt_uniform& u, uint32_t x, uint32
 // 2^-20 relative margin, which bounds |RN(c*rcp(denom)) - RN(c/denom)|.
 __device__ __forceinline__ bool sign_certain_neg(float a, float den)
 {
-    return a != 0.0f && rt_absf(a) >= 0x1p-60f && ((__float_as_uint(a) ^ __float_as_uint(den)) >> 31);
+    return (a != 0.0f) & (rt_absf(a) >= 0x1p-60f) & (((__float_as_uint(a) ^ __float_as_uint(den)) >> 31) != 0u);
 }
 __device__ __forceinline__ bool sign_uncertain(float a) { return a != 0.0f && !(rt_absf(a) >= 0x1p-60f); }
 
@@ -190,14 +190,14 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
     if (FAST) {
         const float tq = c * __builtin_amdgcn_rcpf(denom);
         const float m = rt_absf(tq) * 0x1p-20f + 1e-30f;
-        reject = reject || (rt_absf(denom) <= 0x1p60f && (sign_certain_neg(a, denom) || sign_certain_neg(b, denom) ||
-                                                         tq - m > tmax || tq + m < tmin));
+        reject = reject | ((rt_absf(denom) <= 0x1p60f) & (sign_certain_neg(a, denom) | sign_certain_neg(b, denom) |
+                                                          (tq - m > tmax) | (tq + m < tmin)));
     }
     if (reject) return false;
     beta = a / denom;
     gamma = b / denom;
     dist = c / denom;
-    return !(beta < 0.0f || gamma < 0.0f || beta + gamma > 1.0f || dist > tmax || dist < tmin);
+    return !((beta < 0.0f) | (gamma < 0.0f) | (beta + gamma > 1.0f) | (dist > tmax) | (dist < tmin));
 }
 template <bool FAST>
 __device__ __forceinline__ bool tri_test(const float4* recs, uint32_t k, f3 o, f3 w, float tmin, float tmax,
@@ -299,11 +299,15 @@ __device__ __forceinline__ float4 as_f4(v4u q)
     return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
 }
 
-// One interior-node decision of bsp.wgsl:54-78 at node m (data n).  Returns
-// the next node; pushes {depth(m), t} when both children are visited.
+// One interior-node decision of bsp.wgsl:54-78 at node m (data n, depth dep).
+// Returns the next node.  Branch-free except for the exact division, which
+// only lanes whose approximate t cannot decide near/far take.  The push
+// stores t into the depth-dep slot unconditionally: no pending entry lives at
+// a depth >= depth(m) (they are all ancestors of m), so the store is dead
+// unless the trail bit is set.
 template <bool COUNT>
-__device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, const f3 o, const f3 d,
-                                               const f3 inv, Trav& t, Counters& c)
+__device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, uint32_t dep, const f3 o,
+                                               const f3 d, const f3 inv, Trav& t, Counters& c)
 {
     if (COUNT) c.v[C_INTERIOR]++;
     const uint32_t axis = n.x & 3u;
@@ -312,39 +316,22 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     const float x = __uint_as_float(n.y) - ao;
     const float tq = x * comp(inv, axis);
     const float mg = rt_absf(tq) * 0x1p-20f + 1e-30f;
-    uint32_t next = near_node;
-    if (!(tq - mg > t.tmax)) {   // not certainly t > tmax
-        if (tq + mg < t.tmin && tq + mg <= t.tmax) {   // certainly !(t > tmax) && t < tmin
-            next = near_node ^ 1u;
-        } else {
-            const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
-            const float tt = x / denom;
-            if (!(tt > t.tmax)) {
-                if (tt < t.tmin) {
-                    next = near_node ^ 1u;
-                } else {
-                    const uint32_t dep = heap_depth(m);
-                    stk[dep * 256u] = tt;
-                    t.lvl |= 1u << dep;
-                    t.tmax = tt;
-                }
-            }
-        }
+    // (bitwise & | on bools: no short-circuit control flow)
+    const bool cnear = tq - mg > t.tmax;                                   // certainly t > tmax
+    const bool cfar = (!cnear) & (tq + mg < t.tmin) & (tq + mg <= t.tmax);   // certainly !(t > tmax) && t < tmin
+    const bool amb = (!cnear) & (!cfar);
+    float tt = tq;
+    if (amb) {
+        const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
+        tt = x / denom;
     }
-    return next;
-}
-
-// Node reached by the walk: a leaf starts its triangle range (tested from the
-// next trip on) or, when empty, pops.  Returns true when the ray is finished.
-template <bool COUNT>
-__device__ __forceinline__ bool bsp_leaf(const float* stk, const uint2 n, Trav& t, Counters& c)
-{
-    if (COUNT) c.v[C_LEAF]++;
-    const uint32_t count = n.x >> 2;
-    if (COUNT) c.leafc = count;
-    t.leaf_k = n.y;
-    t.leaf_end = n.y + count;
-    return count == 0u ? bsp_pop(stk, t) : false;
+    const bool inside = amb & !(tt > t.tmax);
+    const bool gofar = cfar | (inside & (tt < t.tmin));
+    const bool push = inside & !(tt < t.tmin);
+    stk[dep * 256u] = tt;
+    t.lvl |= push ? 1u << dep : 0u;
+    t.tmax = push ? tt : t.tmax;
+    return gofar ? near_node ^ 1u : near_node;
 }
 
 // One trip of a lane through intersect_trimesh (bsp.wgsl:10-81).  Every trip
@@ -356,6 +343,8 @@ __device__ __forceinline__ bool bsp_leaf(const float* stk, const uint2 n, Trav& 
 //     quads aligned -- and walks up to three levels with no further load.
 // Nodes and records share one buffer resource, so the four 16-B loads are the
 // same instructions for both kinds of lane (out-of-range offsets read 0).
+// A walk that reaches a leaf starts its triangle range (tested from the next
+// trip on); an empty leaf, or a leaf tested without a hit, pops.
 template <bool COUNT>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
@@ -364,7 +353,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
     const bool in_leaf = t.leaf_k != t.leaf_end;
     const uint32_t rec = S.bsp_rec_off + 48u * t.leaf_k;
-    const uint32_t m = t.node;
+    uint32_t m = t.node;
     const uint32_t o0 = in_leaf ? rec : 8u * (m & ~1u);
     const uint32_t o1 = in_leaf ? rec + 16u : 16u * m;
     const uint32_t o2 = in_leaf ? rec + 32u : 32u * m;
@@ -376,6 +365,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
     // keep the four loads together (the compiler would sink q3 into the
     // level-2 branch: a second round trip)
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+    bool done = false, pop = false;
     if (in_leaf) {
         if (COUNT) {
             c.v[C_IDS]++;
@@ -389,29 +379,41 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             t.hit_k = t.leaf_k;
             t.beta = beta;
             t.gamma = gamma;
-            if (anyhit) return true;
         }
         t.leaf_k++;
-        if (t.leaf_k != t.leaf_end) return false;
-        if (t.found) return true;   // a leaf with an accepted triangle ends the walk
-        return bsp_pop(stk, t);
+        const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
+        done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
+        pop = leaf_done & !t.found;
+    } else {
+        // walk: node m (level 0), a child (level 1), a grandchild (level 2)
+        const uint32_t dep = heap_depth(m);
+        uint2 n = (m & 1u) ? make_uint2(q0.z, q0.w) : make_uint2(q0.x, q0.y);
+        bool leaf = (n.x & 3u) == 3u;
+        if (!leaf) {
+            m = bsp_decide<COUNT>(stk, n, m, dep, o, d, inv, t, c);
+            n = (m & 1u) ? make_uint2(q1.z, q1.w) : make_uint2(q1.x, q1.y);
+            leaf = (n.x & 3u) == 3u;
+            if (!leaf) {
+                m = bsp_decide<COUNT>(stk, n, m, dep + 1u, o, d, inv, t, c);
+                const v4u g = (m & 2u) ? q3 : q2;
+                n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
+                leaf = (n.x & 3u) == 3u;
+                if (!leaf) m = bsp_decide<COUNT>(stk, n, m, dep + 2u, o, d, inv, t, c);
+            }
+        }
+        t.node = m;
+        if (leaf) {
+            if (COUNT) {
+                c.v[C_LEAF]++;
+                c.leafc = n.x >> 2;
+            }
+            t.leaf_k = n.y;
+            t.leaf_end = n.y + (n.x >> 2);
+            pop = (n.x >> 2) == 0u;
+        }
     }
-    // level 0: node m
-    uint2 n = (m & 1u) ? make_uint2(q0.z, q0.w) : make_uint2(q0.x, q0.y);
-    if ((n.x & 3u) == 3u) return bsp_leaf<COUNT>(stk, n, t, c);
-    uint32_t nx = bsp_decide<COUNT>(stk, n, m, o, d, inv, t, c);
-    // level 1: a child of m, from the pair {2m, 2m+1}
-    n = (nx & 1u) ? make_uint2(q1.z, q1.w) : make_uint2(q1.x, q1.y);
-    t.node = nx;
-    if ((n.x & 3u) == 3u) return bsp_leaf<COUNT>(stk, n, t, c);
-    nx = bsp_decide<COUNT>(stk, n, t.node, o, d, inv, t, c);
-    // level 2: a grandchild of m, from the quad {4m .. 4m+3}
-    const v4u g = (nx & 2u) ? q3 : q2;
-    n = (nx & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
-    t.node = nx;
-    if ((n.x & 3u) == 3u) return bsp_leaf<COUNT>(stk, n, t, c);
-    t.node = bsp_decide<COUNT>(stk, n, t.node, o, d, inv, t, c);
-    return false;
+    if (pop) done = bsp_pop(stk, t);
+    return done;
 }
 
 // 1/denom per axis for the approximate interior-node test (denom as bsp.wgsl:63)
