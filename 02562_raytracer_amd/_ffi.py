@@ -10,7 +10,9 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "lib02562rt.so")
+# RT_LIBRARY selects an experimental build variant (see the Makefile knobs);
+# the default is the in-tree library
+LIB_PATH = os.environ.get("RT_LIBRARY") or os.path.join(PKG_DIR, "lib02562rt.so")
 
 RT_OK = 0
 RT_E_INVALID = -1
@@ -62,7 +64,8 @@ class Tileset(C.Structure):
 
 
 COUNT_FIELDS = ["samples", "primary", "shadow", "bounce", "node_interior", "node_leaf", "bvh_pops",
-                "ids_read", "tri_tests", "tri_accepts", "trips", "lane_steps", "leaf_iters", "shade_passes",
+                "ids_read", "tri_tests", "tri_accepts", "trips", "lane_steps", "leaf_lane_steps",
+                "node_trips", "leaf_trips", "exact_tests", "exact_nodes", "shade_passes",
                 "shade_lanes", "trav_cycles", "shade_cycles"]
 
 

@@ -54,7 +54,7 @@ struct rt_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int num_cus = 256;
-    int waves_per_cu = 16;
+    int waves_per_cu = 20;   // 5 waves per SIMD: the k_path register budget (RT_PATH_WAVES_PER_EU)
     int shade_threshold = 32;
     bool detail = false;
     // host copies needed to build the triangle records on BSP/BVH upload

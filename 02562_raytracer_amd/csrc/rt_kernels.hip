@@ -73,11 +73,11 @@ __device__ __forceinline__ float rnd(uint32_t& prev) { return (float)mcg31(prev)
 
 // ------------------------------------------------------------------ counters
 enum { C_SAMPLES, C_PRIMARY, C_SHADOW, C_BOUNCE, C_INTERIOR, C_LEAF, C_POPS, C_IDS, C_TESTS, C_ACCEPTS,
-       C_TRIPS, C_LANE_STEPS, C_LEAF_ITERS, C_SHADE_PASSES, C_SHADE_LANES, C_TRAV_CYC64, C_SHADE_CYC64, C_N };
+       C_TRIPS, C_LANE_STEPS, C_LEAF_LANE_STEPS, C_NODE_TRIPS, C_LEAF_TRIPS, C_EXACT_TESTS, C_EXACT_NODES,
+       C_SHADE_PASSES, C_SHADE_LANES, C_TRAV_CYC64, C_SHADE_CYC64, C_N };
 
 struct Counters {
     uint32_t v[C_N];
-    uint32_t leafc;   // diagnostics: triangles in the leaf this lane visited this trip
 };
 
 __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long long* out, bool detail)
@@ -174,9 +174,9 @@ __device__ __forceinline__ bool sign_certain_neg(float a, float den)
 }
 __device__ __forceinline__ bool sign_uncertain(float a) { return a != 0.0f && !(rt_absf(a) >= 0x1p-60f); }
 
-template <bool FAST>
+template <bool FAST, bool COUNT = false>
 __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const float4 r2, f3 o, f3 w, float tmin,
-                                         float tmax, float& dist, float& beta, float& gamma)
+                                         float tmax, float& dist, float& beta, float& gamma, Counters* cn = nullptr)
 {
     const f3 v0 = V(r0.x, r0.y, r0.z), e0 = V(r0.w, r1.x, r1.y), e1 = V(r1.z, r1.w, r2.x);
     const f3 n = V(r2.y, r2.z, r2.w);
@@ -194,6 +194,7 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
                                                           (tq - m > tmax) | (tq + m < tmin)));
     }
     if (reject) return false;
+    if (COUNT) cn->v[C_EXACT_TESTS]++;
     beta = a / denom;
     gamma = b / denom;
     dist = c / denom;
@@ -322,6 +323,7 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     const bool amb = (!cnear) & (!cfar);
     float tt = tq;
     if (amb) {
+        if (COUNT) c.v[C_EXACT_NODES]++;
         const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
         tt = x / denom;
     }
@@ -372,7 +374,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             c.v[C_TESTS]++;
         }
         float dist, beta, gamma;
-        if (tri_math<true>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma)) {
+        if (tri_math<true, COUNT>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
@@ -405,7 +407,6 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
         if (leaf) {
             if (COUNT) {
                 c.v[C_LEAF]++;
-                c.leafc = n.x >> 2;
             }
             t.leaf_k = n.y;
             t.leaf_end = n.y + (n.x >> 2);
@@ -471,7 +472,6 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
         const float4 a = S.bvh_nodes[2u * cur], b = S.bvh_nodes[2u * cur + 1u];
         if (bb2(inv, o, a, b)) {
             const uint32_t off = __float_as_uint(a.w), np = __float_as_uint(b.w);
-            if (COUNT) c.leafc = np;
             if (np > 0u) {
                 t.leaf_k = off;
                 t.leaf_end = off + np;
@@ -634,8 +634,14 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 // needs the two possible contributions (visible / blocked), the RR decision
 // and the next direction, all computed with the same operations in the same
 // PRNG order before the shadow ray is traced.
+// Occupancy target (waves per SIMD): the register budget the compiler fits the
+// path kernel into (5 -> <= 96 VGPRs; spills, if any, stay in the shading code).
+#ifndef RT_PATH_WAVES_PER_EU
+#define RT_PATH_WAVES_PER_EU 5
+#endif
 template <int MODE, int TRAV, bool COUNT>
-__global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PATH_WAVES_PER_EU, 8)))
+k_path(DevScene S, DevLaunch L)
 {
     extern __shared__ uint32_t lds_stack[];   // [level][thread], 4 B entries
     void* stk = lds_stack + threadIdx.x;
@@ -695,19 +701,22 @@ __global__ void __launch_bounds__(256) k_path(DevScene S, DevLaunch L)
             const uint64_t trm = __ballot(alive && tracing);
             const uint64_t wtm = __ballot(alive && !tracing);
             if (!(trm != 0 && (wtm == 0 || T >= 64u || (uint32_t)__popcll(trm) > T))) break;
-            if (COUNT) cnt.leafc = 0;
-            if (alive && tracing) {
-                if (COUNT) cnt.v[C_LANE_STEPS]++;
-                if (trav_step<TRAV, COUNT>(S, stk, ro, rd, inv, shadow, tr, cnt)) tracing = false;
-            }
             if (COUNT) {
-                uint32_t mx = cnt.leafc;
-#pragma unroll
-                for (int off = 32; off > 0; off >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, off, 64));
+                const bool leafst = tr.leaf_k != tr.leaf_end;
+                const uint64_t nm = __ballot(alive && tracing && !leafst);
+                const uint64_t lm = __ballot(alive && tracing && leafst);
+                if (alive && tracing) {
+                    cnt.v[C_LANE_STEPS]++;
+                    if (leafst) cnt.v[C_LEAF_LANE_STEPS]++;
+                }
                 if (lane == 0) {
                     cnt.v[C_TRIPS]++;
-                    cnt.v[C_LEAF_ITERS] += mx;
+                    cnt.v[C_NODE_TRIPS] += nm != 0;
+                    cnt.v[C_LEAF_TRIPS] += lm != 0;
                 }
+            }
+            if (alive && tracing) {
+                if (trav_step<TRAV, COUNT>(S, stk, ro, rd, inv, shadow, tr, cnt)) tracing = false;
             }
         }
         if (COUNT) {

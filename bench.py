@@ -217,9 +217,10 @@ def main():
             "cpu_baseline": cpu,
             "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},
             "traversal_per_launch": {k: detail[k] for k in ("node_interior", "node_leaf", "bvh_pops", "tri_tests",
-                                                            "tri_accepts", "trips", "lane_steps", "leaf_iters",
-                                                            "shade_passes", "shade_lanes", "trav_cycles",
-                                                            "shade_cycles")},
+                                                            "tri_accepts", "trips", "lane_steps",
+                                                            "leaf_lane_steps", "node_trips", "leaf_trips",
+                                                            "exact_tests", "exact_nodes", "shade_passes",
+                                                            "shade_lanes", "trav_cycles", "shade_cycles")},
             "simd_lane_util": round(detail["lane_steps"] / max(1, 64 * detail["trips"]), 4),
             "setup_s": round(setup_s, 3),
         }

@@ -134,7 +134,11 @@ typedef struct rt_ray_counts {
      * of the traversal loop: */
     uint64_t trips;          /* traversal loop trips (sum over waves)      */
     uint64_t lane_steps;     /* lanes that advanced a ray in those trips    */
-    uint64_t leaf_iters;     /* leaf-loop iterations executed (wave level) */
+    uint64_t leaf_lane_steps;/* ... of which were inside a leaf (triangle)  */
+    uint64_t node_trips;     /* trips in which some lane walked nodes       */
+    uint64_t leaf_trips;     /* trips in which some lane tested a triangle  */
+    uint64_t exact_tests;    /* triangle tests that needed exact division   */
+    uint64_t exact_nodes;    /* node decisions that needed exact division   */
     /* path kernels, per wave: shading passes, lanes shaded, and wave cycles
      * (s_memtime) spent in the traversal and in the shading/refill phases */
     uint64_t shade_passes;
@@ -145,7 +149,7 @@ typedef struct rt_ray_counts {
 
 /* ---- options (rt_set_option) ------------------------------------------- */
 #define RT_OPT_DETAIL_COUNTERS 1  /* 0/1: use the counting kernel instantiation    */
-#define RT_OPT_WAVES_PER_CU    2  /* persistent grid size: waves per CU (default 16) */
+#define RT_OPT_WAVES_PER_CU    2  /* persistent grid size: waves per CU (default 20) */
 #define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace; 64 = all lanes finish their rays first (lockstep) */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */

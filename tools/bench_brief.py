@@ -8,7 +8,12 @@ trips = max(1, t["trips"])
 cyc = max(1, t.get("trav_cycles", 0) + t.get("shade_cycles", 0))
 print(f'{d["value"]} Mrays/s  {d["ms_per_step"]} ms/step  kernel {d["roofline"]["kernel_ms"]} ms  '
       f'frac {d["roofline"]["frac"]}  lane_util {d["simd_lane_util"]}  '
-      f'leaf_iters/trip {t["leaf_iters"] / trips:.3f}  trips {trips:.3e}  '
+      f'trips {trips:.3e}  node_trips {t.get("node_trips", 0) / trips:.3f}  '
+      f'leaf_trips {t.get("leaf_trips", 0) / trips:.3f}  '
+      f'node_lanes/trip {(t["lane_steps"] - t.get("leaf_lane_steps", 0)) / trips:.1f}  '
+      f'leaf_lanes/trip {t.get("leaf_lane_steps", 0) / trips:.1f}  '
+      f'exact_tests/test {t.get("exact_tests", 0) / max(1, t["tri_tests"]):.3f}  '
+      f'exact_nodes/node {t.get("exact_nodes", 0) / max(1, t["node_interior"]):.3f}  '
       f'shade_passes/trip {t.get("shade_passes", 0) / trips:.3f}  '
       f'shade_lanes/pass {t.get("shade_lanes", 0) / max(1, t.get("shade_passes", 0)):.1f}  '
       f'trav_cycle_frac {t.get("trav_cycles", 0) / cyc:.3f}  '
