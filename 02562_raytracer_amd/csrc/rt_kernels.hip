@@ -188,10 +188,17 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
     const float c = dot(ov, n);
     bool reject = rt_absf(denom) < 1e-10f;
     if (FAST) {
-        const float tq = c * __builtin_amdgcn_rcpf(denom);
+        // certain rejections, each implying the exact predicate below rejects:
+        // a sign (beta < 0 / gamma < 0), the distance range, or
+        // RN(beta + gamma) > 1 (needs beta + gamma > 1 + 2^-24: margin 2^-22)
+        const float r = __builtin_amdgcn_rcpf(denom);
+        const float tq = c * r;
         const float m = rt_absf(tq) * 0x1p-20f + 1e-30f;
+        const float qa = a * r, qb = b * r;
+        const float ms = (rt_absf(qa) + rt_absf(qb)) * 0x1p-20f;
         reject = reject | ((rt_absf(denom) <= 0x1p60f) & (sign_certain_neg(a, denom) | sign_certain_neg(b, denom) |
-                                                          (tq - m > tmax) | (tq + m < tmin)));
+                                                          (tq - m > tmax) | (tq + m < tmin) |
+                                                          (qa + qb - ms > 1.0f + 0x1p-22f)));
     }
     if (reject) return false;
     if (COUNT) cn->v[C_EXACT_TESTS]++;
@@ -312,10 +319,10 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 {
     if (COUNT) c.v[C_INTERIOR]++;
     const uint32_t axis = n.x & 3u;
-    const float ad = comp(d, axis), ao = comp(o, axis);
-    const uint32_t near_node = 2u * m + (ad >= 0.0f ? 0u : 1u);
+    const float ao = comp(o, axis), iv = comp(inv, axis);
+    const uint32_t near_node = 2u * m + (__float_as_uint(iv) >> 31);   // see bsp_inv1
     const float x = __uint_as_float(n.y) - ao;
-    const float tq = x * comp(inv, axis);
+    const float tq = x * iv;
     const float mg = rt_absf(tq) * 0x1p-20f + 1e-30f;
     // (bitwise & | on bools: no short-circuit control flow)
     const bool cnear = tq - mg > t.tmax;                                   // certainly t > tmax
@@ -324,6 +331,7 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     float tt = tq;
     if (amb) {
         if (COUNT) c.v[C_EXACT_NODES]++;
+        const float ad = comp(d, axis);
         const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
         tt = x / denom;
     }
@@ -417,13 +425,19 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
     return done;
 }
 
-// 1/denom per axis for the approximate interior-node test (denom as bsp.wgsl:63)
-__device__ __forceinline__ f3 bsp_inv(const f3 d)
+// 1/denom per axis for the approximate interior-node test (denom as bsp.wgsl:63).
+// Its sign bit also carries the near-child choice (`dir[axis] >= 0` -> left,
+// bsp.wgsl:54-60): the two disagree only when dir[axis] is a negative value
+// of magnitude < 1e-8 (denom is +1e-8 there) or NaN; those components get a
+// negative NaN, which sends every decision on that axis to the exact path
+// (NaN compares false) with the right near child.
+__device__ __forceinline__ float bsp_inv1(float ad)
 {
-    return V(__builtin_amdgcn_rcpf(rt_absf(d.x) < 1.0e-8f ? 1.0e-8f : d.x),
-             __builtin_amdgcn_rcpf(rt_absf(d.y) < 1.0e-8f ? 1.0e-8f : d.y),
-             __builtin_amdgcn_rcpf(rt_absf(d.z) < 1.0e-8f ? 1.0e-8f : d.z));
+    const float r = __builtin_amdgcn_rcpf(rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad);
+    const bool near_right = !(ad >= 0.0f);
+    return (near_right && !(__float_as_uint(r) >> 31)) ? __uint_as_float(0xFFC00000u) : r;
 }
+__device__ __forceinline__ f3 bsp_inv(const f3 d) { return V(bsp_inv1(d.x), bsp_inv1(d.y), bsp_inv1(d.z)); }
 
 // ------------------------------------------------------------------ BVH traversal
 // intersect_bvh + intersect_bb2, bvh.wgsl:154-191 / 16-83: slab test in axis

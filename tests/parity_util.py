@@ -34,10 +34,11 @@ class Scene:
         self.oscene = O.SceneRef(self.om, self.obsp, self.obvh, env)
 
     def render_gpu(self, mode, cam, W, H, region, first_iter=0, spp=1, selection1=0, accum_in=None,
-                   tileset=None):
+                   tileset=None, jitter=None):
         rt, ctx = self.rt, self.ctx
-        u = rt.make_uniform(*cam, W, H, selection1=selection1)
-        ctx.set_uniforms(u)
+        subdiv = 1 if jitter is None else int(round(np.sqrt(len(jitter))))
+        u = rt.make_uniform(*cam, W, H, selection1=selection1, subdiv=subdiv)
+        ctx.set_uniforms(u, None if jitter is None else np.ascontiguousarray(jitter, dtype=np.float32))
         x0, y0, w, h = region
         acc = ctx.alloc(w * h * 16)
         ids = ctx.alloc(w * h * 4)
@@ -53,9 +54,11 @@ class Scene:
         return a, i, cnt
 
     def render_oracle(self, mode, cam, W, H, region, first_iter=0, spp=1, selection1=0, accum_in=None,
-                      nthreads=None):
-        u = O.make_uniform(*cam, W, H, selection1=selection1)
-        return O.render(self.oscene, u, mode, self.trav, region, first_iter, spp, accum=accum_in, nthreads=nthreads)
+                      nthreads=None, jitter=None):
+        subdiv = 1 if jitter is None else int(round(np.sqrt(len(jitter))))
+        u = O.make_uniform(*cam, W, H, selection1=selection1, subdiv=subdiv)
+        return O.render(self.oscene, u, mode, self.trav, region, first_iter, spp, accum=accum_in, nthreads=nthreads,
+                        jitter=None if jitter is None else np.ascontiguousarray(jitter, dtype=np.float32))
 
 
 def compare(gpu, ora, what=""):

@@ -88,6 +88,23 @@ def test_primary_modes(rt, gpu, mode, trav, name):
     check(g, o)
 
 
+@pytest.mark.parametrize("mode,trav", [("W6E1", "BSP"), ("PROJECT", "BSP"), ("PROJECT", "BVH")])
+def test_axis_aligned_and_tiny_direction_components(rt, gpu, mode, trav):
+    """An axis-aligned camera and a hand-made jitter table (uniform.rs:254-277
+    jitter[] with subdivision 2) put exact zeros, tiny negatives (|d| < 1e-8:
+    bsp.wgsl:63 divides by +1e-8 while the near child follows the sign) and
+    near-threshold values into ray directions around the centre pixel."""
+    cam = ((0.0, 1.5, 10.0), (0.0, 1.5, 0.0), (0.0, 1.0, 0.0), 2.5)
+    W, H = 801, 451                         # odd: the centre pixel has uv = (0, 0)
+    jitter = [(0.0, 0.0), (-1e-9, 1e-9), (-2e-8, -3e-9), (1e-10, -5e-9)]
+    s = Scene(rt, rt.Mesh.from_obj(model("teapot.obj")), trav)
+    region = (368, 209, 64, 32)
+    g = s.render_gpu(mode, cam, W, H, region, jitter=jitter)
+    o = s.render_oracle(mode, cam, W, H, region, jitter=jitter)
+    check(g, o)
+    assert (g[1] != 0xFFFFFFFF).any()
+
+
 @pytest.mark.parametrize("sel", [2, 5, 6, 4])
 def test_shader_selection(rt, gpu, sel):
     # uniforms.selection1 switch of shade(): mirror, normal, base colour, default (error colour)
