@@ -55,7 +55,7 @@ struct rt_ctx {
     std::string err;
     int num_cus = 256;
     int waves_per_cu = 20;   // 5 waves per SIMD: the k_path register budget (RT_PATH_WAVES_PER_EU)
-    int shade_threshold = 32;
+    int shade_threshold = 40;
     bool detail = false;
     // host copies needed to build the triangle records on BSP/BVH upload
     std::vector<float> h_pos;
