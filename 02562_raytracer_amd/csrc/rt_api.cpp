@@ -369,15 +369,6 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
         if (ids[k] >= c->ntris) return fail(c, RT_E_INVALID, "rt_upload_bsp: triangle id out of range");
     // validate the reachable tree (implicit children, leaves inside ids)
     std::vector<uint32_t> stack{0};
-    // 8-B device nodes, 1-based heap order: slot 0 is padding, node i at slot i+1
-    // (the kernel walks 1-based indices; sibling pairs 2M, 2M+1 share 16 B)
-    std::vector<uint32_t> packed(((size_t)nnodes + 1) * 2, 0u);
-    for (uint32_t i = 0; i < nnodes; i++) {
-        packed[2 * ((size_t)i + 1)] = tree[4 * (size_t)i];
-        uint32_t pbits;
-        memcpy(&pbits, &planes[i], 4);
-        packed[2 * ((size_t)i + 1) + 1] = (tree[4 * (size_t)i] & 3u) == 3u ? tree[4 * (size_t)i + 1] : pbits;
-    }
     while (!stack.empty()) {
         const uint32_t i = stack.back();
         stack.pop_back();
@@ -385,6 +376,8 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
         if ((n[0] & 3u) == 3u) {
             if ((uint64_t)n[1] + (n[0] >> 2) > nids)
                 return fail(c, RT_E_INVALID, "rt_upload_bsp: leaf range outside treeIds");
+            if ((n[0] >> 2) >= (1u << 24))
+                return fail(c, RT_E_UNSUPPORTED, "rt_upload_bsp: leaf with 2^24 or more triangles");
             continue;
         }
         const uint64_t l = 2ull * i + 1, rgt = 2ull * i + 2;
@@ -399,20 +392,50 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_bsp = false;
     int r;
-    // one allocation [nodes | records]: the kernel reads both through one buffer
-    // resource with 32-bit offsets (node treelets and triangle records are
-    // fetched by the same loads, DESIGN.md "Data layout in HBM")
-    const size_t node_bytes = (packed.size() * 4 + 255) & ~(size_t)255;
-    const size_t total = node_bytes + recs.size() * 4;
-    if (total >= ((size_t)1 << 32) || (size_t)nnodes * 32 + 64 >= ((size_t)1 << 32))
-        return fail(c, RT_E_UNSUPPORTED, "rt_upload_bsp: BSP nodes + records must stay below 4 GiB (max_depth <= 26)");
+    // One allocation [treelets | records], read through one buffer resource
+    // with 32-bit offsets (DESIGN.md "Data layout in HBM"):
+    //  * treelet of node M (1-based heap index), 64 B at 64*M: the 8-B nodes
+    //    {M, 2M | 2M+1, pad | 4M, 4M+1 | 4M+2, 4M+3} -- everything a 3-level walk
+    //    from M reads, in one 64-B line;
+    //  * 8-B node: interior {axis, plane bits}; leaf {3 | (48*count) << 2, byte
+    //    offset of its first record} (children implicit: 2i+1, 2i+2 0-based);
+    //  * record k (treeIds slot k): 48 B {v0, e0, e1, n} at rec_off + 48*k.
+    const size_t slots = (size_t)nnodes + 1;
+    const size_t rec_off = (slots * 64 + 255) & ~(size_t)255;
+    const size_t total = rec_off + recs.size() * 4;
+    if (total >= ((size_t)1 << 32))
+        return fail(c, RT_E_UNSUPPORTED, "rt_upload_bsp: BSP treelets + records must stay below 4 GiB (max_depth <= 24)");
     {
+        auto node8 = [&](size_t m, uint32_t* o) {   // 1-based m; zero beyond the tree
+            if (m == 0 || m > nnodes) {
+                o[0] = o[1] = 0u;
+                return;
+            }
+            const uint32_t* n = tree + 4 * (m - 1);
+            if ((n[0] & 3u) == 3u) {
+                o[0] = 3u | ((48u * (n[0] >> 2)) << 2);
+                o[1] = (uint32_t)(rec_off + 48ull * n[1]);
+            } else {
+                o[0] = n[0] & 3u;
+                memcpy(&o[1], &planes[m - 1], 4);
+            }
+        };
         std::vector<uint8_t> blob(total, 0);
-        memcpy(blob.data(), packed.data(), packed.size() * 4);
-        memcpy(blob.data() + node_bytes, recs.data(), recs.size() * 4);
+        uint32_t* tl = reinterpret_cast<uint32_t*>(blob.data());
+        for (size_t m = 1; m < slots; m++) {
+            uint32_t* o = tl + 16 * m;
+            node8(m, o);
+            node8(2 * m, o + 2);
+            node8(2 * m + 1, o + 4);
+            node8(4 * m, o + 8);
+            node8(4 * m + 1, o + 10);
+            node8(4 * m + 2, o + 12);
+            node8(4 * m + 3, o + 14);
+        }
+        memcpy(blob.data() + rec_off, recs.data(), recs.size() * 4);
         if ((r = upload(c, c->bsp_nodes, blob.data(), blob.size()))) return r;
     }
-    c->bsp_rec_off = (uint32_t)node_bytes;
+    c->bsp_rec_off = (uint32_t)rec_off;
     if ((r = upload(c, c->bsp_ids, ids, (size_t)nids * 4))) return r;
     c->bsp_depth = max_depth;
     c->aabb[0] = aabb[0];

@@ -17,10 +17,12 @@ struct DevScene {
     const rt_material* mats;
     const uint32_t* lights;
     uint32_t nverts, ntris, nmats, nlights;
-    // BSP: 8-byte nodes {x = axis|count<<2, y = plane bits (interior) / first id (leaf)}, 1-based (slot 0 pad);
-    // children implicit (2i+1, 2i+2, src/data_structures/bsp_tree.rs:137-140).
-    const uint2* bsp_nodes;       // start of one allocation [nodes | records]
-    const float4* bsp_recs;       // 3 x float4 per treeIds slot: v0, e0=v1-v0, e1=v2-v0, n=cross(e0,e1)
+    // BSP: one allocation [64-B treelets | 48-B records] (rt_api.cpp rt_upload_bsp):
+    // treelet of 1-based node M at 64*M holds nodes M, 2M, 2M+1, 4M..4M+3 (8 B each:
+    // interior {axis, plane bits}, leaf {3 | (48*count) << 2, first record's byte offset});
+    // children implicit (2i+1, 2i+2 0-based, src/data_structures/bsp_tree.rs:137-140).
+    const uint2* bsp_nodes;       // start of the allocation
+    const float4* bsp_recs;       // = bsp_nodes + bsp_rec_off: v0, e0=v1-v0, e1=v2-v0, n=cross(e0,e1)
     uint32_t bsp_bytes;           // size of the allocation (buffer-resource range)
     uint32_t bsp_rec_off;         // byte offset of the records
     const uint32_t* bsp_ids;      // treeIds

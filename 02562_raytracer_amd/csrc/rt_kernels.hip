@@ -288,7 +288,8 @@ __device__ __forceinline__ void leaf_test(const float4* recs, const f3 o, const 
 // boolean, and the walk up to that triangle is identical, so it is too.
 // Interior nodes: the exact t = RN((plane - o)/denom) is only divided out when
 // the approximate t (v_rcp_f32, 2^-20 margin) cannot decide near/far.
-__device__ __forceinline__ uint32_t heap_depth(uint32_t m) { return 31u - (uint32_t)__clz((int)m); }
+// m >= 1 always (a zero argument would be undefined: no clamp instruction)
+__device__ __forceinline__ uint32_t heap_depth(uint32_t m) { return 31u - (uint32_t)__builtin_clz(m); }
 
 __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 {
@@ -344,17 +345,17 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     return gofar ? near_node ^ 1u : near_node;
 }
 
-// One trip of a lane through intersect_trimesh (bsp.wgsl:10-81).  Every trip
-// issues its loads together, before any decision (one memory round trip):
-//   * a lane inside a leaf tests one triangle: its 48-B record;
-//   * a lane walking nodes fetches the 3-level treelet below its node m:
-//     the 16 B holding node m, the sibling pair {2m, 2m+1} (16 B) and the
-//     grandchildren {4m..4m+3} (32 B) -- 1-based heap order keeps pairs and
-//     quads aligned -- and walks up to three levels with no further load.
-// Nodes and records share one buffer resource, so the four 16-B loads are the
-// same instructions for both kinds of lane (out-of-range offsets read 0).
+// One trip of a lane through intersect_trimesh (bsp.wgsl:10-81).  Every lane
+// issues the same four 16-B loads at one base offset, before any decision
+// (one memory round trip per trip):
+//   * a lane inside a leaf tests one triangle: base = its 48-B record;
+//   * a lane walking nodes reads the 64-B treelet of its node m (rt_api.cpp:
+//     nodes m | 2m, 2m+1 | 4m..4m+3) and walks up to three levels with no
+//     further load.
+// Treelets and records share one buffer resource (out-of-range reads are 0).
 // A walk that reaches a leaf starts its triangle range (tested from the next
-// trip on); an empty leaf, or a leaf tested without a hit, pops.
+// trip on); an empty leaf, or a leaf tested without a hit, pops.  Leaf ranges
+// (leaf_k, leaf_end, hit_k) are byte offsets of records in that buffer.
 template <bool COUNT>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
@@ -362,17 +363,13 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
     const bool in_leaf = t.leaf_k != t.leaf_end;
-    const uint32_t rec = S.bsp_rec_off + 48u * t.leaf_k;
     uint32_t m = t.node;
-    const uint32_t o0 = in_leaf ? rec : 8u * (m & ~1u);
-    const uint32_t o1 = in_leaf ? rec + 16u : 16u * m;
-    const uint32_t o2 = in_leaf ? rec + 32u : 32u * m;
-    const uint32_t o3 = in_leaf ? 0xFFFFFFF0u : 32u * m + 16u;
-    v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, o0, 0, 0);
-    v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, o1, 0, 0);
-    v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, o2, 0, 0);
-    v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, o3, 0, 0);
-    // keep the four loads together (the compiler would sink q3 into the
+    const uint32_t base = in_leaf ? t.leaf_k : m << 6;
+    v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
+    v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
+    v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
+    v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 48u, 0, 0);
+    // keep the four loads together (the compiler would sink q2/q3 into the
     // level-2 branch: a second round trip)
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
     bool done = false, pop = false;
@@ -390,18 +387,18 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             t.beta = beta;
             t.gamma = gamma;
         }
-        t.leaf_k++;
+        t.leaf_k += 48u;
         const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
         done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
         pop = leaf_done & !t.found;
     } else {
         // walk: node m (level 0), a child (level 1), a grandchild (level 2)
         const uint32_t dep = heap_depth(m);
-        uint2 n = (m & 1u) ? make_uint2(q0.z, q0.w) : make_uint2(q0.x, q0.y);
+        uint2 n = make_uint2(q0.x, q0.y);
         bool leaf = (n.x & 3u) == 3u;
         if (!leaf) {
             m = bsp_decide<COUNT>(stk, n, m, dep, o, d, inv, t, c);
-            n = (m & 1u) ? make_uint2(q1.z, q1.w) : make_uint2(q1.x, q1.y);
+            n = (m & 1u) ? make_uint2(q1.x, q1.y) : make_uint2(q0.z, q0.w);
             leaf = (n.x & 3u) == 3u;
             if (!leaf) {
                 m = bsp_decide<COUNT>(stk, n, m, dep + 1u, o, d, inv, t, c);
@@ -413,11 +410,9 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
         }
         t.node = m;
         if (leaf) {
-            if (COUNT) {
-                c.v[C_LEAF]++;
-            }
+            if (COUNT) c.v[C_LEAF]++;
             t.leaf_k = n.y;
-            t.leaf_end = n.y + (n.x >> 2);
+            t.leaf_end = n.y + (n.x >> 2);   // 48 * count
             pop = (n.x >> 2) == 0u;
         }
     }
@@ -551,14 +546,17 @@ __device__ __forceinline__ HitRec resolve(const DevScene& S, const TraceOut& t, 
                                           bool face_normals)
 {
     HitRec h;
-    const uint32_t* ids = TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids;
-    const float4* recs = TRAV == RT_TRAVERSE_BVH ? S.bvh_recs : S.bsp_recs;
-    h.tri = ids[t.k];
+    // BSP: t.k is the record's byte offset in the treelet+record buffer
+    const uint32_t slot = TRAV == RT_TRAVERSE_BVH ? t.k : (t.k - S.bsp_rec_off) / 48u;
+    const float4* r2p = TRAV == RT_TRAVERSE_BVH
+                            ? S.bvh_recs + 3u * t.k + 2u
+                            : reinterpret_cast<const float4*>(reinterpret_cast<const uint8_t*>(S.bsp_nodes) + t.k + 32u);
+    h.tri = (TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids)[slot];
     const uint4 ix = S.tri_idx[h.tri];
     h.pos = add(o, muls(d, t.dist));
     f3 n0, n1, n2;
     if (face_normals) {
-        const float4 r2 = recs[3u * t.k + 2u];
+        const float4 r2 = *r2p;
         n0 = n1 = n2 = V(r2.y, r2.z, r2.w);
     } else {
         n0 = ld3(S.nrm[ix.x]);
@@ -675,7 +673,10 @@ k_path(DevScene S, DevLaunch L)
 #pragma unroll
     for (int i = 0; i < C_N; i++) cnt.v[i] = 0;
 
-    bool alive = false, tracing = false, exhausted = L.spp == 0u, shadow = false, emit = true, survive = false;
+    // lane state: ST_IDLE (no pixel), ST_TRACE (a ray in flight), ST_SHADE (ray done, waiting to shade)
+    enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2 };
+    uint32_t st = ST_IDLE;
+    bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false;
     uint32_t px = 0, py = 0, out = 0, it = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
     float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
     f3 res = V(0, 0, 0), fac = V(1, 1, 1), ro = V(0, 0, 0), rd = V(0, 0, 1), inv = V(0, 0, 0);
@@ -702,7 +703,7 @@ k_path(DevScene S, DevLaunch L)
         shadow = false;
         inv = trav_inv<TRAV>(rd);
         trav_start<TRAV>(tr, stk, ETA, 5000.0f);
-        tracing = true;
+        st = ST_TRACE;
         cnt.v[C_SAMPLES]++;
         cnt.v[C_PRIMARY]++;
     };
@@ -712,14 +713,14 @@ k_path(DevScene S, DevLaunch L)
         // ---- traversal phase: every tracing lane advances its ray by one node
         //      visit / triangle test per trip, until enough lanes wait to shade
         for (;;) {
-            const uint64_t trm = __ballot(alive && tracing);
-            const uint64_t wtm = __ballot(alive && !tracing);
+            const uint64_t trm = __ballot(st == ST_TRACE);
+            const uint64_t wtm = __ballot(st == ST_SHADE);
             if (!(trm != 0 && (wtm == 0 || T >= 64u || (uint32_t)__popcll(trm) > T))) break;
             if (COUNT) {
                 const bool leafst = tr.leaf_k != tr.leaf_end;
-                const uint64_t nm = __ballot(alive && tracing && !leafst);
-                const uint64_t lm = __ballot(alive && tracing && leafst);
-                if (alive && tracing) {
+                const uint64_t nm = __ballot(st == ST_TRACE && !leafst);
+                const uint64_t lm = __ballot(st == ST_TRACE && leafst);
+                if (st == ST_TRACE) {
                     cnt.v[C_LANE_STEPS]++;
                     if (leafst) cnt.v[C_LEAF_LANE_STEPS]++;
                 }
@@ -729,8 +730,8 @@ k_path(DevScene S, DevLaunch L)
                     cnt.v[C_LEAF_TRIPS] += lm != 0;
                 }
             }
-            if (alive && tracing) {
-                if (trav_step<TRAV, COUNT>(S, stk, ro, rd, inv, shadow, tr, cnt)) tracing = false;
+            if (st == ST_TRACE) {
+                if (trav_step<TRAV, COUNT>(S, stk, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }
         }
         if (COUNT) {
@@ -739,11 +740,11 @@ k_path(DevScene S, DevLaunch L)
                 cnt.v[C_TRAV_CYC64] += (uint32_t)((now - tstamp) >> 6);
                 cnt.v[C_SHADE_PASSES]++;
             }
-            if (alive && !tracing) cnt.v[C_SHADE_LANES]++;
+            if (st == ST_SHADE) cnt.v[C_SHADE_LANES]++;
             tstamp = now;
         }
         // ---- shading phase
-        if (alive && !tracing) {
+        if (st == ST_SHADE) {
             bool sample_done = false;
             if (!shadow) {
                 if (tr.found) {
@@ -781,7 +782,7 @@ k_path(DevScene S, DevLaunch L)
                         inv = trav_inv<TRAV>(rd);
                         trav_start<TRAV>(tr, stk, ETA, Lt.dist - ETA);
                         shadow = true;
-                        tracing = true;
+                        st = ST_TRACE;
                         cnt.v[C_SHADOW]++;
                     } else if (sel == 2u) {
                         // mirror (w9e1.wgsl:491-504): reflect, offset origin, emit = true
@@ -793,7 +794,7 @@ k_path(DevScene S, DevLaunch L)
                             bounce++;
                             inv = trav_inv<TRAV>(rd);
                             trav_start<TRAV>(tr, stk, ETA, 5000.0f);
-                            tracing = true;
+                            st = ST_TRACE;
                             cnt.v[C_BOUNCE]++;
                         } else {
                             sample_done = true;
@@ -821,7 +822,7 @@ k_path(DevScene S, DevLaunch L)
                     emit = false;
                     bounce++;
                     shadow = false;
-                    tracing = true;
+                    st = ST_TRACE;
                     cnt.v[C_BOUNCE]++;
                 } else {
                     sample_done = true;
@@ -839,19 +840,19 @@ k_path(DevScene S, DevLaunch L)
                 } else {
                     L.accum[out] = make_float4(a0, a1, a2, 1.0f);
                     if (L.ids) L.ids[out] = prim;
-                    alive = false;
+                    st = ST_IDLE;
                 }
             }
         }
         // ---- refill idle lanes with new pixels (ballot + mbcnt compaction)
         for (;;) {
-            const uint64_t need = __ballot(!alive && !exhausted);
+            const uint64_t need = __ballot(st == ST_IDLE && !exhausted);
             if (need == 0) break;
             const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need) - 1u;
             uint32_t base = 0;
             if (lane == leader) base = atomicAdd(L.work_counter, (uint32_t)__popcll(need));
             base = __shfl(base, (int)leader, 64);
-            if (!alive && !exhausted) {
+            if (st == ST_IDLE && !exhausted) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
                 const uint32_t slot = base + rank;
@@ -871,7 +872,6 @@ k_path(DevScene S, DevLaunch L)
                             a1 = pa.y;
                             a2 = pa.z;
                         }
-                        alive = true;
                         start_sample();
                     }
                 }
@@ -882,7 +882,7 @@ k_path(DevScene S, DevLaunch L)
             if (lane == 0) cnt.v[C_SHADE_CYC64] += (uint32_t)((now - tstamp) >> 6);
             tstamp = now;
         }
-        if (__ballot(alive) == 0) break;
+        if (__ballot(st != ST_IDLE) == 0) break;
     }
     flush_counters(cnt, L.counters, COUNT);
 }
