@@ -66,7 +66,7 @@ class Tileset(C.Structure):
 COUNT_FIELDS = ["samples", "primary", "shadow", "bounce", "node_interior", "node_leaf", "bvh_pops",
                 "ids_read", "tri_tests", "tri_accepts", "trips", "lane_steps", "leaf_lane_steps",
                 "node_trips", "leaf_trips", "exact_tests", "exact_nodes", "shade_passes",
-                "shade_lanes", "trav_cycles", "shade_cycles"]
+                "shade_lanes", "trav_cycles", "shade_cycles", "memwait_cycles"]
 
 
 class RayCounts(C.Structure):

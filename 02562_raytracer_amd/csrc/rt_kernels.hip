@@ -74,7 +74,7 @@ __device__ __forceinline__ float rnd(uint32_t& prev) { return (float)mcg31(prev)
 // ------------------------------------------------------------------ counters
 enum { C_SAMPLES, C_PRIMARY, C_SHADOW, C_BOUNCE, C_INTERIOR, C_LEAF, C_POPS, C_IDS, C_TESTS, C_ACCEPTS,
        C_TRIPS, C_LANE_STEPS, C_LEAF_LANE_STEPS, C_NODE_TRIPS, C_LEAF_TRIPS, C_EXACT_TESTS, C_EXACT_NODES,
-       C_SHADE_PASSES, C_SHADE_LANES, C_TRAV_CYC64, C_SHADE_CYC64, C_N };
+       C_SHADE_PASSES, C_SHADE_LANES, C_TRAV_CYC64, C_SHADE_CYC64, C_MEMWAIT_CYC64, C_N };
 
 struct Counters {
     uint32_t v[C_N];
@@ -86,7 +86,8 @@ __device__ __forceinline__ void flush_counters(const Counters& c, unsigned long 
     for (int i = 0; i < n; i++) {
         uint32_t x = c.v[i];
         unsigned long long s = x;
-        if (i == C_TRAV_CYC64 || i == C_SHADE_CYC64) s <<= 6;   // wave cycles, accumulated in units of 64
+        if (i == C_TRAV_CYC64 || i == C_SHADE_CYC64 || i == C_MEMWAIT_CYC64)
+            s <<= 6;   // wave cycles, accumulated in units of 64
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
         if ((threadIdx.x & 63u) == 0 && s) atomicAdd(out + i, s);
@@ -286,8 +287,8 @@ __device__ __forceinline__ void leaf_test(const float4* recs, const f3 o, const 
 // walk ends.
 // anyhit: stop at the first accepted triangle -- shadow rays use only the
 // boolean, and the walk up to that triangle is identical, so it is too.
-// Interior nodes: the exact t = RN((plane - o)/denom) is only divided out when
-// the approximate t (v_rcp_f32, 2^-20 margin) cannot decide near/far.
+// Interior nodes: the exact t = RN((plane - o)/denom) is only derived when the
+// approximate t (x * RN(1/denom), 2^-20 margin) cannot decide near/far.
 // m >= 1 always (a zero argument would be undefined: no clamp instruction)
 __device__ __forceinline__ uint32_t heap_depth(uint32_t m) { return 31u - (uint32_t)__builtin_clz(m); }
 
@@ -334,7 +335,10 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
         if (COUNT) c.v[C_EXACT_NODES]++;
         const float ad = comp(d, axis);
         const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
-        tt = x / denom;
+        // RN(x / denom) from the per-ray RN(1/denom) (include/rt_detmath.h);
+        // IEEE division outside its operand range or for a NaN-flagged axis
+        if (rt_div_by_recip_ok(x) & (iv == iv)) tt = rt_div_by_recip(x, denom, iv);
+        else tt = x / denom;
     }
     const bool inside = amb & !(tt > t.tmax);
     const bool gofar = cfar | (inside & (tt < t.tmin));
@@ -365,6 +369,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
     const bool in_leaf = t.leaf_k != t.leaf_end;
     uint32_t m = t.node;
     const uint32_t base = in_leaf ? t.leaf_k : m << 6;
+    uint64_t tw = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
     v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
     v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
@@ -372,6 +377,11 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
     // keep the four loads together (the compiler would sink q2/q3 into the
     // level-2 branch: a second round trip)
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+    if (COUNT) {   // diagnostics: cycles from issuing the loads to their data
+        tw = __builtin_amdgcn_s_memtime() - tw;
+        if ((threadIdx.x & 63u) == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u))
+            c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
+    }
     bool done = false, pop = false;
     if (in_leaf) {
         if (COUNT) {
@@ -420,7 +430,8 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
     return done;
 }
 
-// 1/denom per axis for the approximate interior-node test (denom as bsp.wgsl:63).
+// RN(1/denom) per axis (denom as bsp.wgsl:63): the approximate interior-node
+// test multiplies by it, and the exact t is derived from it (rt_div_by_recip).
 // Its sign bit also carries the near-child choice (`dir[axis] >= 0` -> left,
 // bsp.wgsl:54-60): the two disagree only when dir[axis] is a negative value
 // of magnitude < 1e-8 (denom is +1e-8 there) or NaN; those components get a
@@ -428,7 +439,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
 // (NaN compares false) with the right near child.
 __device__ __forceinline__ float bsp_inv1(float ad)
 {
-    const float r = __builtin_amdgcn_rcpf(rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad);
+    const float r = 1.0f / (rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad);   // RN(1/denom): rt_div_by_recip's reciprocal
     const bool near_right = !(ad >= 0.0f);
     return (near_right && !(__float_as_uint(r) >> 31)) ? __uint_as_float(0xFFC00000u) : r;
 }
@@ -1165,6 +1176,9 @@ __host__ __device__ inline void math_eval(float x, float* o)
     o[5] = (x * 3.0f + 1.0f) / (x - 7.0f);
     o[6] = (float)(uint32_t)((x < 0.0f ? -x : x) * 1000.0f) / (float)0x80000000u;
     o[7] = rt_det_acosf(rt_det_sqrtf(1.0f - (x - __builtin_floorf(x))));
+    const float dd = 0.13f + (x < 0.0f ? -x : x) * 0.2f, xx = x * 37.1f + 0.3f;   // the BSP walk's fast exact division
+    o[8] = rt_div_by_recip(xx, dd, 1.0f / dd);
+    o[9] = xx / dd;
 }
 __global__ void k_selftest_math(const float* in, float* out, uint32_t n)
 {

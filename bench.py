@@ -220,7 +220,8 @@ def main():
                                                             "tri_accepts", "trips", "lane_steps",
                                                             "leaf_lane_steps", "node_trips", "leaf_trips",
                                                             "exact_tests", "exact_nodes", "shade_passes",
-                                                            "shade_lanes", "trav_cycles", "shade_cycles")},
+                                                            "shade_lanes", "trav_cycles", "shade_cycles",
+                                                            "memwait_cycles")},
             "simd_lane_util": round(detail["lane_steps"] / max(1, 64 * detail["trips"]), 4),
             "setup_s": round(setup_s, 3),
         }

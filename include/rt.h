@@ -145,6 +145,7 @@ typedef struct rt_ray_counts {
     uint64_t shade_lanes;
     uint64_t trav_cycles;
     uint64_t shade_cycles;
+    uint64_t memwait_cycles; /* BSP trips: wave cycles from load issue to data */
 } rt_ray_counts;
 
 /* ---- options (rt_set_option) ------------------------------------------- */

@@ -29,6 +29,23 @@
 
 RT_HD float rt_det_sqrtf(float x) { return __builtin_sqrtf(x); }
 
+/* Correctly rounded x / d from r = RN(1/d) (Markstein's theorem: with y within
+ * 1/2 ulp of 1/d and q within 1 ulp of x/d, RN(q + (x - d*q)*y) == RN(x/d); the
+ * first correction brings RN(x*r), up to 2 ulp off, within 1 ulp).  Exact when
+ * d is a finite normal number, r == RN(1/d) and 2^-100 <= |x| <= 2^100 with
+ * |x/d| < 2^127 (no overflow, and every residual representable); callers use
+ * x / d outside that range.  tests/test_fastdiv.py checks it bitwise against
+ * IEEE division on ~10^8 operand pairs. */
+RT_HD float rt_div_by_recip(float x, float d, float r)
+{
+    float q = x * r;
+    float e = __builtin_fmaf(-d, q, x);
+    q = __builtin_fmaf(e, r, q);
+    e = __builtin_fmaf(-d, q, x);
+    return __builtin_fmaf(e, r, q);
+}
+RT_HD int rt_div_by_recip_ok(float x) { float a = __builtin_fabsf(x); return a >= 0x1p-100f && a <= 0x1p100f; }
+
 /* WGSL min/max/saturate/sign on f32 are implementation-defined for NaN and
  * for the sign of zero; these are the pinned choices (ternaries, so the host
  * libm and the GPU min/max instructions cannot disagree on +-0). */

@@ -17,4 +17,5 @@ print(f'{d["value"]} Mrays/s  {d["ms_per_step"]} ms/step  kernel {d["roofline"][
       f'shade_passes/trip {t.get("shade_passes", 0) / trips:.3f}  '
       f'shade_lanes/pass {t.get("shade_lanes", 0) / max(1, t.get("shade_passes", 0)):.1f}  '
       f'trav_cycle_frac {t.get("trav_cycles", 0) / cyc:.3f}  '
-      f'cycles/trip {t.get("trav_cycles", 0) / trips:.0f}  wave_Gcycles {cyc / 1e9:.1f}')
+      f'cycles/trip {t.get("trav_cycles", 0) / trips:.0f}  memwait/trip {t.get("memwait_cycles", 0) / trips:.0f}  '
+      f'wave_Gcycles {cyc / 1e9:.1f}')
