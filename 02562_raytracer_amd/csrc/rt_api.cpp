@@ -68,7 +68,8 @@ struct rt_ctx {
     uint32_t bsp_depth = 0;
     float aabb[6] = {0, 0, 0, 0, 0, 0};
     bool has_bsp = false;
-    DevBuf bvh_nodes, bvh_recs, bvh_ids;
+    DevBuf bvh_nodes, bvh_ids;   // bvh_nodes: [32-B nodes | 48-B records]
+    uint32_t bvh_rec_off = 0;
     uint32_t bvh_nnodes = 0;
     bool has_bvh = false;
     rt_uniform u;
@@ -479,8 +480,33 @@ int rt_upload_bvh(rt_ctx* c, const rt_gpu_node* nodes, uint32_t nnodes, const ui
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_bvh = false;
     int r;
-    if ((r = upload(c, c->bvh_nodes, nodes, (size_t)nnodes * sizeof(rt_gpu_node)))) return r;
-    if ((r = upload(c, c->bvh_recs, recs.data(), recs.size() * 4))) return r;
+    // One allocation [32-B node records | 48-B triangle records], read through
+    // one buffer resource with 32-bit offsets.  Node record: {min.xyz, w0}
+    // {max.xyz, w1}; interior: w0 = byte offset of the right child (offset_ptr),
+    // w1 = 0; leaf: w0 = byte offset of its first triangle record, w1 = 48*n_prims.
+    const size_t rec_off = ((size_t)nnodes * 32 + 255) & ~(size_t)255;
+    const size_t total = rec_off + recs.size() * 4;
+    if (total >= ((size_t)1 << 32))
+        return fail(c, RT_E_UNSUPPORTED, "rt_upload_bvh: BVH nodes + records must stay below 4 GiB");
+    {
+        std::vector<uint8_t> blob(total, 0);
+        for (uint32_t i = 0; i < nnodes; i++) {
+            const rt_gpu_node& n = nodes[i];
+            uint32_t* o = reinterpret_cast<uint32_t*>(blob.data() + 32 * (size_t)i);
+            memcpy(o, n.min, 12);
+            memcpy(o + 4, n.max, 12);
+            if (n.n_prims > 0) {
+                o[3] = (uint32_t)(rec_off + 48ull * n.offset_ptr);
+                o[7] = 48u * n.n_prims;
+            } else {
+                o[3] = (uint32_t)(32ull * n.offset_ptr);
+                o[7] = 0u;
+            }
+        }
+        memcpy(blob.data() + rec_off, recs.data(), recs.size() * 4);
+        if ((r = upload(c, c->bvh_nodes, blob.data(), blob.size()))) return r;
+    }
+    c->bvh_rec_off = (uint32_t)rec_off;
     if ((r = upload(c, c->bvh_ids, tri_ids, (size_t)nids * 4))) return r;
     c->bvh_nnodes = nnodes;
     c->has_bvh = true;
@@ -551,8 +577,9 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     S.bsp_ids = c->bsp_ids.as<uint32_t>();
     S.bsp_depth = c->bsp_depth;
     memcpy(S.aabb, c->aabb, sizeof S.aabb);
-    S.bvh_nodes = c->bvh_nodes.as<float4>();
-    S.bvh_recs = c->bvh_recs.as<float4>();
+    S.bvh_base = c->bvh_nodes.as<uint8_t>();
+    S.bvh_bytes = (uint32_t)c->bvh_nodes.n;
+    S.bvh_rec_off = c->bvh_rec_off;
     S.bvh_ids = c->bvh_ids.as<uint32_t>();
     S.bvh_nnodes = c->bvh_nnodes;
     L.u = c->u;

@@ -28,9 +28,11 @@ struct DevScene {
     const uint32_t* bsp_ids;      // treeIds
     uint32_t bsp_depth;           // MAX_LEVEL
     float aabb[6];                // root BboxGpu min.xyz, max.xyz
-    // BVH: GpuNode as 2 x float4; records in bvh_triangles order
-    const float4* bvh_nodes;
-    const float4* bvh_recs;
+    // BVH: one allocation [32-B node records | 48-B triangle records in bvh_triangles
+    // order] (rt_api.cpp rt_upload_bvh; links and leaf ranges as byte offsets)
+    const uint8_t* bvh_base;
+    uint32_t bvh_bytes;
+    uint32_t bvh_rec_off;
     const uint32_t* bvh_ids;
     uint32_t bvh_nnodes;
 };

@@ -208,16 +208,6 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
     dist = c / denom;
     return !((beta < 0.0f) | (gamma < 0.0f) | (beta + gamma > 1.0f) | (dist > tmax) | (dist < tmin));
 }
-template <bool FAST>
-__device__ __forceinline__ bool tri_test(const float4* recs, uint32_t k, f3 o, f3 w, float tmin, float tmax,
-                                         float& dist, float& beta, float& gamma)
-{
-    // all three 16-B pieces are loaded before the first decision, so a test
-    // costs one memory round trip (an early |denom| exit would let the
-    // compiler sink the r0/r1 loads behind the r2 load)
-    return tri_math<FAST>(recs[3u * k], recs[3u * k + 1u], recs[3u * k + 2u], o, w, tmin, tmax, dist, beta, gamma);
-}
-
 struct TraceOut {
     uint32_t k;   // record slot of the accepted triangle
     float beta, gamma, dist;
@@ -234,6 +224,7 @@ struct Trav {
     bool found;
     uint32_t hit_k;
     float beta, gamma;
+    uint32_t tos;    // BVH: cached top-of-stack value (node byte offset)
 };
 
 __device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
@@ -247,26 +238,6 @@ __device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
     t.found = false;
 }
 __device__ __forceinline__ TraceOut trav_out(const Trav& t) { return TraceOut{t.hit_k, t.beta, t.gamma, t.tmax}; }
-
-// One triangle test of the current leaf (shared by BSP and BVH).
-template <bool COUNT>
-__device__ __forceinline__ void leaf_test(const float4* recs, const f3 o, const f3 d, Trav& t, Counters& c)
-{
-    if (COUNT) {
-        c.v[C_IDS]++;
-        c.v[C_TESTS]++;
-    }
-    float dist, beta, gamma;
-    if (tri_test<true>(recs, t.leaf_k, o, d, t.tmin, t.tmax, dist, beta, gamma)) {
-        if (COUNT) c.v[C_ACCEPTS]++;
-        t.tmax = dist;
-        t.found = true;
-        t.hit_k = t.leaf_k;
-        t.beta = beta;
-        t.gamma = gamma;
-    }
-    t.leaf_k++;
-}
 
 // ------------------------------------------------------------------ BSP traversal
 // intersect_trimesh, bsp.wgsl:10-81, as a per-lane state machine: each call
@@ -471,43 +442,75 @@ __device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, co
     return !(t0 > t1);
 }
 
-__device__ __forceinline__ void bvh_init(Trav& t, uint32_t* stk, float tmin, float tmax)
+__device__ __forceinline__ void bvh_init(Trav& t, float tmin, float tmax)
 {
     trav_init(t, tmin, tmax);
-    stk[0] = 0u;   // stack_push_node(0u)
-    t.node = 1;    // top
-    t.lvl = 0;     // pops
+    t.node = 1;     // top: stack_push_node(0u)
+    t.lvl = 0;      // pops
+    t.tos = 0u;     // the root's byte offset, cached top of stack
 }
 
+// One trip of a lane through intersect_bvh (bvh.wgsl:154-191), one memory
+// round trip: a lane inside a leaf tests one triangle (its 48-B record), a
+// lane between leaves pops one node (32-B record) and slab-tests it.  The
+// stack holds node byte offsets in LDS ([slot][thread], slot = min(i, 49):
+// WGSL index clamping) with its top value cached in a register (t.tos), so a
+// pop needs no LDS read before the node load; the next top is read from LDS
+// for the following trip.  Device node records (rt_api.cpp rt_upload_bvh):
+// {min.xyz, w0}{max.xyz, w1}, interior w0 = byte offset of the right child
+// (the left child is the next record), w1 = 0; leaf w0 = byte offset of its
+// first triangle record, w1 = 48 * n_prims.
 template <bool COUNT>
 __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
 {
-    if (t.leaf_k == t.leaf_end) {
-        if (t.lvl >= 1000u || t.node == 0u) return true;
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)S.bvh_base, (short)0, (int)S.bvh_bytes, 0x00020000);
+    const bool in_leaf = t.leaf_k != t.leaf_end;
+    const uint32_t base = in_leaf ? t.leaf_k : t.tos;
+    v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
+    v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
+    v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
+    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2));
+    if (in_leaf) {
+        if (COUNT) {
+            c.v[C_IDS]++;
+            c.v[C_TESTS]++;
+        }
+        float dist, beta, gamma;
+        if (tri_math<true, COUNT>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+            if (COUNT) c.v[C_ACCEPTS]++;
+            t.tmax = dist;
+            t.found = true;
+            t.hit_k = t.leaf_k;
+            t.beta = beta;
+            t.gamma = gamma;
+        }
+        t.leaf_k += 48u;
+        if (anyhit & t.found) return true;
+    } else {
+        if (COUNT) c.v[C_POPS]++;
         t.lvl++;
         t.node--;
-        const uint32_t cur = stk[(t.node < 50u ? t.node : 49u) * 256u];
-        if (COUNT) c.v[C_POPS]++;
-        const float4 a = S.bvh_nodes[2u * cur], b = S.bvh_nodes[2u * cur + 1u];
-        if (bb2(inv, o, a, b)) {
-            const uint32_t off = __float_as_uint(a.w), np = __float_as_uint(b.w);
-            if (np > 0u) {
-                t.leaf_k = off;
-                t.leaf_end = off + np;
-            } else {
-                stk[(t.node < 50u ? t.node : 49u) * 256u] = cur + 1u;
-                t.node++;
-                stk[(t.node < 50u ? t.node : 49u) * 256u] = off;
-                t.node++;
-            }
+        const uint32_t cur = t.tos;
+        const float4 a = as_f4(q0), b = as_f4(q1);
+        const bool hit = bb2(inv, o, a, b);
+        const uint32_t w0 = q0.w, w1 = q1.w;
+        if (hit & (w1 != 0u)) {   // leaf: its triangles from the next trip on
+            t.leaf_k = w0;
+            t.leaf_end = w0 + w1;
         }
-        if (t.leaf_k == t.leaf_end) return t.lvl >= 1000u || t.node == 0u;
+        if (hit & (w1 == 0u)) {   // interior: push left (cur + 1), then right
+            stk[(t.node < 50u ? t.node : 49u) * 256u] = cur + 32u;
+            t.node++;
+            stk[(t.node < 50u ? t.node : 49u) * 256u] = w0;
+            t.node++;
+            t.tos = w0;
+        } else if (t.node != 0u) {
+            t.tos = stk[(t.node - 1u < 50u ? t.node - 1u : 49u) * 256u];
+        }
     }
-    leaf_test<COUNT>(S.bvh_recs, o, d, t, c);
-    if (t.found && anyhit) return true;
-    if (t.leaf_k != t.leaf_end) return false;
-    return t.lvl >= 1000u || t.node == 0u;
+    return (t.leaf_k == t.leaf_end) & ((t.lvl >= 1000u) | (t.node == 0u));
 }
 
 // The 1/d of bvh.wgsl:155 (exact division: it feeds the slab test directly).
@@ -521,7 +524,7 @@ __device__ __forceinline__ f3 trav_inv(const f3 d)
 template <int TRAV>
 __device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float tmax)
 {
-    if (TRAV == RT_TRAVERSE_BVH) bvh_init(t, reinterpret_cast<uint32_t*>(stk), tmin, tmax);
+    if (TRAV == RT_TRAVERSE_BVH) bvh_init(t, tmin, tmax);
     else trav_init(t, tmin, tmax);
 }
 template <int TRAV, bool COUNT>
@@ -557,11 +560,10 @@ __device__ __forceinline__ HitRec resolve(const DevScene& S, const TraceOut& t, 
                                           bool face_normals)
 {
     HitRec h;
-    // BSP: t.k is the record's byte offset in the treelet+record buffer
-    const uint32_t slot = TRAV == RT_TRAVERSE_BVH ? t.k : (t.k - S.bsp_rec_off) / 48u;
-    const float4* r2p = TRAV == RT_TRAVERSE_BVH
-                            ? S.bvh_recs + 3u * t.k + 2u
-                            : reinterpret_cast<const float4*>(reinterpret_cast<const uint8_t*>(S.bsp_nodes) + t.k + 32u);
+    // t.k is the record's byte offset in the node+record buffer of the traversal
+    const uint8_t* base = TRAV == RT_TRAVERSE_BVH ? S.bvh_base : reinterpret_cast<const uint8_t*>(S.bsp_nodes);
+    const uint32_t slot = (t.k - (TRAV == RT_TRAVERSE_BVH ? S.bvh_rec_off : S.bsp_rec_off)) / 48u;
+    const float4* r2p = reinterpret_cast<const float4*>(base + t.k + 32u);
     h.tri = (TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids)[slot];
     const uint4 ix = S.tri_idx[h.tri];
     h.pos = add(o, muls(d, t.dist));
