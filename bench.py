@@ -2,16 +2,18 @@
 path at 1920x1080, 256 spp (BASELINE.json configs[2]: ~70k-tri bunny, W9E1
 path tracer), on N GPUs of one node.
 
-One step = one complete 1920x1080 x 256-spp progressive frame (iterations
-0..255, the reference's 256 RenderState::render() calls fused into one launch
-per GPU) with the framebuffer tiled across ranks (interleaved 8x8 tiles) and
-the finished tiles all-gathered over RCCL to assemble the frame on rank 0.
+One step = one complete progressive frame (iterations 0..spp-1, the
+reference's spp RenderState::render() calls fused into one launch per GPU)
+with the framebuffer tiled across ranks (interleaved 8x8 tiles) and the
+finished tiles all-gathered over RCCL to assemble the frame on rank 0.
 Total work is fixed as N grows ("strong" scaling).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config 2..5]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.  See DESIGN.md "Measurement".
+--config selects another BASELINE.json workload (02562_raytracer_amd/configs.py);
+the default, 3, is the headline.  Prints ONE JSON line on rank 0.  See
+DESIGN.md "Measurement".
 """
 import argparse
 import importlib
@@ -42,18 +44,25 @@ def algorithmic_bytes(c, trav, npix, first_iter):
     return t + fb
 
 
-def cpu_baseline(args, mesh, cam, W, H, budget_s):
+def cpu_baseline(wl, trav, mesh, accel, spp, W, H, budget_s):
     """The CPU oracle (a restatement of the reference WGSL path; the reference
     itself needs Rust + Vulkan, absent here) on the host cores, over a bounded
     sample of the same workload: the full frame, 1 spp per pass, passes
-    (iterations 0, 1, 2, ...) repeated until ~budget_s of CPU time."""
+    (iterations 0, 1, 2, ...) repeated until ~budget_s of CPU time.  The oracle
+    renders from the product builder's arrays (bit-identical to the oracle's own
+    builders: tests/test_host_builders.py), which spares its single-threaded
+    BSP build on the 7M/10M-triangle configs."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_ffi as O
     V, N, I, M, L = mesh.arrays()
     om = O.OracleMesh(V, N, I, M, L)
-    osc = O.SceneRef(om, O.build_bsp(om) if args.trav == "BSP" else None,
-                     O.build_bvh(om) if args.trav == "BVH" else None, env=(1.0, 1.0, 1.0))
-    u = O.make_uniform(*cam, W, H)
+    if trav == "BSP":
+        tree, planes, ids, aabb, md = accel.arrays()
+        osc = O.SceneRef(om, O.OracleBsp(tree, planes, ids, aabb, md), None, env=wl.env)
+    else:
+        nodes, tids = accel.arrays()
+        osc = O.SceneRef(om, None, O.OracleBvh(nodes, tids), env=wl.env)
+    u = O.make_uniform(*wl.camera, W, H)
     cores = min(16, os.cpu_count() or 1)
     region = (0, 0, W, H)
     acc = None
@@ -61,15 +70,15 @@ def cpu_baseline(args, mesh, cam, W, H, budget_s):
     it = 0
     t0 = time.perf_counter()
     while True:
-        acc, _, c = O.render(osc, u, "W9E1", args.trav, region, it, 1, accum=acc, nthreads=cores)
+        acc, _, c = O.render(osc, u, wl.mode, trav, region, it, 1, accum=acc, nthreads=cores)
         rays += c["primary"] + c["shadow"]
         it += 1
         el = time.perf_counter() - t0
-        if el >= budget_s or it >= args.spp:
+        if el >= budget_s or it >= spp:
             break
     return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"CPU oracle (C restatement of w9e1.wgsl+bsp.wgsl, pthreads), the same {W}x{H} frame, "
-                      f"first {it} of its {args.spp} spp, {el:.1f} s"}
+            "sample": f"CPU oracle (C restatement of {wl.mode.lower()}.wgsl+{trav.lower()}.wgsl, pthreads), the same "
+                      f"{W}x{H} frame, first {it} of its {spp} spp, {el:.1f} s"}
 
 
 def main():
@@ -77,11 +86,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=256)
-    ap.add_argument("--width", type=int, default=1920)
-    ap.add_argument("--height", type=int, default=1080)
-    ap.add_argument("--trav", default="BSP", choices=["BSP", "BVH"])
-    ap.add_argument("--ntris", type=int, default=69451)
+    ap.add_argument("--config", type=int, default=3, choices=[2, 3, 4, 5])
+    ap.add_argument("--spp", type=int, default=None)
+    ap.add_argument("--width", type=int, default=None)
+    ap.add_argument("--height", type=int, default=None)
+    ap.add_argument("--trav", default=None, choices=["BSP", "BVH"])
+    ap.add_argument("--ntris", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shade-threshold", type=int, default=None)
@@ -106,11 +116,14 @@ def main():
 
     rt = importlib.import_module("02562_raytracer_amd")   # after torch: shares its HIP runtime
     tiling = importlib.import_module("02562_raytracer_amd.tiling")
-    W, H = args.width, args.height
-    cam = ((-0.02, 0.11, 0.6), (-0.02, 0.11, 0.0), (0.0, 1.0, 0.0), 3.5)   # scenes.rs:71-77
+    wl = importlib.import_module("02562_raytracer_amd.configs").WORKLOADS[args.config]
+    W, H = args.width or wl.width, args.height or wl.height
+    spp = args.spp or wl.spp
+    trav = args.trav or wl.traversal
+    cam = wl.camera
 
     t0 = time.perf_counter()
-    mesh = rt.Mesh.synth_bunny(args.ntris)
+    mesh = wl.mesh(args.ntris)
     ctx = rt.Context(local)
     ctx.set_stream(stream.cuda_stream)
     if args.shade_threshold is not None:
@@ -118,13 +131,13 @@ def main():
     if args.waves_per_cu is not None:
         ctx.set_option(rt._ffi.RT_OPT_WAVES_PER_CU, args.waves_per_cu)
     ctx.upload_mesh(mesh)
-    if args.trav == "BSP":
+    if trav == "BSP":
         accel = mesh.bsp_tree()
         ctx.upload_bsp(accel)
     else:
         accel = mesh.bvh()
         ctx.upload_bvh(accel)
-    ctx.set_environment((1.0, 1.0, 1.0))
+    ctx.set_environment(wl.env)
     ctx.set_uniforms(rt.make_uniform(*cam, W, H, selection1=0))
     setup_s = time.perf_counter() - t0
 
@@ -140,7 +153,7 @@ def main():
     def step(events=None):
         if events is not None:
             events[0].record(stream)
-        ctx.render_tiles("W9E1", args.trav, rank, world, 0, args.spp, acc_local.data_ptr(), ids_local.data_ptr())
+        ctx.render_tiles(wl.mode, trav, rank, world, 0, spp, acc_local.data_ptr(), ids_local.data_ptr())
         if events is not None:
             events[1].record(stream)
         if world > 1:
@@ -164,7 +177,7 @@ def main():
         step()
 
     rays = torch.tensor([counts["primary"] + counts["shadow"], counts["primary"], counts["shadow"],
-                         counts["bounce"], algorithmic_bytes(detail, args.trav, lt * 64, 0)],
+                         counts["bounce"], algorithmic_bytes(detail, trav, lt * 64, 0)],
                         dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(rays)
@@ -189,7 +202,7 @@ def main():
 
     value = rays[0] * args.steps / elapsed / 1e6
     if rank == 0:
-        # roofline of the dominant kernel (k_path W9E1 BSP): bytes of one launch
+        # roofline of the dominant kernel (k_path<mode, traversal>): bytes of one launch
         # on one GPU / its average HIP-event duration
         bytes_per_launch = rays[4] / world
         achieved = bytes_per_launch / (kern_ms / 1e3) / 1e9
@@ -198,21 +211,22 @@ def main():
         if os.path.exists(pmc):
             with open(pmc) as f:
                 p = json.load(f)
-            key = f"{W}x{H}x{args.spp}_{args.trav}_n{world}"
+            key = f"{W}x{H}x{spp}_{trav}_n{world}" + ("" if args.config == 3 else f"_c{args.config}")
             traffic = p.get(key)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
-            cpu = cpu_baseline(args, mesh, cam, W, H, args.cpu_budget)
+            cpu = cpu_baseline(wl, trav, mesh, accel, spp, W, H, args.cpu_budget)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": f"bunny stand-in ({mesh.ntris} tris) W9E1 path trace, {args.trav} D20/leaf4, "
-                                   f"{W}x{H}, {args.spp} spp/step", "resolution": [W, H], "spp": args.spp,
-                       "traversal": args.trav, "ntris": mesh.ntris, "parallelism": f"tiles8x8/{world}"},
+            "config": {"workload": f"config {wl.number}: {wl.name} ({mesh.ntris} tris), "
+                                   f"{trav}{' D20/leaf4' if trav == 'BSP' else ' leaf4'}, {W}x{H}, {spp} spp/step",
+                       "resolution": [W, H], "spp": spp, "traversal": trav, "ntris": mesh.ntris, "mode": wl.mode,
+                       "parallelism": f"tiles8x8/{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_path<W9E1,BSP>", "kernel_ms": round(kern_ms, 3),
+                         "kernel": f"k_path<{wl.mode},{trav}>", "kernel_ms": round(kern_ms, 3),
                          "algorithmic_bytes_per_launch": int(bytes_per_launch)},
             "cpu_baseline": cpu,
             "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},

@@ -16,7 +16,11 @@ class Scene:
     uploads its own (rt.Mesh -> BspTree/Bvh -> Context), the oracle builds its
     own from the same triangle arrays."""
 
-    def __init__(self, rt, mesh, trav, env=(1.0, 1.0, 1.0), oracle_mesh=None, device=0):
+    def __init__(self, rt, mesh, trav, env=(1.0, 1.0, 1.0), oracle_mesh=None, device=0, oracle_accel_from_product=False):
+        """oracle_accel_from_product: the oracle renders from the product
+        builder's arrays instead of building its own (they are bit-identical,
+        tests/test_host_builders.py) -- for the 7M/10M-triangle configs, where
+        the single-threaded oracle build would dominate the test."""
         ctx = rt.Context(device)   # one context per scene: uploads never clobber another test's scene
         self.rt, self.ctx, self.trav, self.env = rt, ctx, trav, env
         self.mesh = mesh
@@ -25,11 +29,13 @@ class Scene:
         ctx.upload_mesh(mesh)
         self.obsp = self.obvh = None
         if trav == "BSP":
-            ctx.upload_bsp(mesh.bsp_tree())
-            self.obsp = O.build_bsp(self.om)
+            bsp = mesh.bsp_tree()
+            ctx.upload_bsp(bsp)
+            self.obsp = O.OracleBsp(*bsp.arrays()) if oracle_accel_from_product else O.build_bsp(self.om)
         elif trav == "BVH":
-            ctx.upload_bvh(mesh.bvh())
-            self.obvh = O.build_bvh(self.om)
+            bvh = mesh.bvh()
+            ctx.upload_bvh(bvh)
+            self.obvh = O.OracleBvh(*bvh.arrays()) if oracle_accel_from_product else O.build_bvh(self.om)
         ctx.set_environment(env)
         self.oscene = O.SceneRef(self.om, self.obsp, self.obvh, env)
 
