@@ -27,6 +27,10 @@ RT_TRAVERSE_BSP, RT_TRAVERSE_BVH, RT_TRAVERSE_NONE = range(3)
 RT_OPT_DETAIL_COUNTERS = 1
 RT_OPT_WAVES_PER_CU = 2
 RT_OPT_SHADE_THRESHOLD = 3
+RT_OPT_SAMPLE_CHUNK = 4
+RT_OPT_SAMPLE_BUDGET_MB = 5
+RT_OPT_UNIT_ORDER = 6
+RT_OPT_KERNEL_TIMING = 7
 
 MODES = {"W1E6": RT_MODE_W1E6, "W6E1": RT_MODE_W6E1, "PROJECT": RT_MODE_PROJECT, "W7E3": RT_MODE_W7E3,
          "W9E1": RT_MODE_W9E1}
@@ -108,6 +112,7 @@ SIGNATURES = {
     "rt_memset_device": (C.c_int, [vp, vp, C.c_int, C.c_size_t]),
     "rt_timer_start": (C.c_int, [vp]),
     "rt_timer_stop": (C.c_int, [vp, f32p]),
+    "rt_kernel_time": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), u32p]),
     "rt_upload_mesh": (C.c_int, [vp, f32p, f32p, C.c_uint32, u32p, C.c_uint32, C.POINTER(Material), C.c_uint32,
                                  u32p, C.c_uint32]),
     "rt_upload_bsp": (C.c_int, [vp, f32p, u32p, f32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32]),

@@ -343,6 +343,14 @@ class Context:
         self._chk(F.lib().rt_timer_stop(self._h, C.byref(ms)))
         return ms.value
 
+    def kernel_time(self, reset=True):
+        """(summed ms, launches) of the traversal-kernel launches timed since the
+        last reset (RT_OPT_KERNEL_TIMING must be on); synchronizes."""
+        ms = C.c_double()
+        n = C.c_uint32()
+        self._chk(F.lib().rt_kernel_time(self._h, int(reset), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
     def selftest_math(self, n=1 << 20, lo=-4.0, hi=4.0):
         bad = C.c_uint32()
         self._chk(F.lib().rt_selftest_math(self._h, n, lo, hi, C.byref(bad)))

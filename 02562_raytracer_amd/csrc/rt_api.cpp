@@ -55,7 +55,11 @@ struct rt_ctx {
     std::string err;
     int num_cus = 256;
     int waves_per_cu = 20;   // 5 waves per SIMD: the k_path register budget (RT_PATH_WAVES_PER_EU)
-    int shade_threshold = 40;
+    int shade_threshold = 8;    // with pixel-major units: lanes refill together (coherent samples)
+    uint32_t sample_chunk = 1;          // iterations per k_path work unit
+    uint32_t unit_order = 1;            // 0: chunk-major, 1: pixel-major
+    uint64_t sample_budget_mb = 16384;  // per-sample scratch (one pass at 1080p x 256 spp needs 8.1 GiB)
+    DevBuf samples;
     bool detail = false;
     // host copies needed to build the triangle records on BSP/BVH upload
     std::vector<float> h_pos;
@@ -80,6 +84,10 @@ struct rt_ctx {
     DevBuf work, counters;
     rt_ray_counts last;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    // RT_OPT_KERNEL_TIMING: event pairs around traversal-kernel launches (pool reused after reset)
+    bool ktiming = false;
+    std::vector<hipEvent_t> kev;
+    size_t kused = 0;   // events recorded since the last reset (2 per launch)
 };
 
 namespace {
@@ -202,6 +210,7 @@ void rt_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
+    for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -239,6 +248,21 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
     case RT_OPT_SHADE_THRESHOLD:
         if (value < 0 || value > 64) return fail(c, RT_E_INVALID, "shade threshold must be in [0,64] (64 = lockstep)");
         c->shade_threshold = (int)value;
+        return RT_OK;
+    case RT_OPT_SAMPLE_CHUNK:
+        if (value < 1 || value > (1 << 20)) return fail(c, RT_E_INVALID, "sample chunk must be in [1,2^20]");
+        c->sample_chunk = (uint32_t)value;
+        return RT_OK;
+    case RT_OPT_KERNEL_TIMING:
+        c->ktiming = value != 0;
+        return RT_OK;
+    case RT_OPT_UNIT_ORDER:
+        if (value < 0 || value > 1) return fail(c, RT_E_INVALID, "unit order must be 0 or 1");
+        c->unit_order = (uint32_t)value;
+        return RT_OK;
+    case RT_OPT_SAMPLE_BUDGET_MB:
+        if (value < 1 || value > (1 << 20)) return fail(c, RT_E_INVALID, "sample budget must be in [1,2^20] MiB");
+        c->sample_budget_mb = (uint64_t)value;
         return RT_OK;
     default:
         return fail(c, RT_E_INVALID, "unknown option");
@@ -301,6 +325,23 @@ int rt_timer_start(rt_ctx* c)
         HIPCHK(c, hipEventCreate(&c->ev1));
     }
     HIPCHK(c, hipEventRecord(c->ev0, c->stream));
+    return RT_OK;
+}
+
+int rt_kernel_time(rt_ctx* c, int reset, double* total_ms, uint32_t* launches)
+{
+    if (!c) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    double tot = 0.0;
+    for (size_t i = 0; i + 1 < c->kused; i += 2) {
+        HIPCHK(c, hipEventSynchronize(c->kev[i + 1]));
+        float ms = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&ms, c->kev[i], c->kev[i + 1]));
+        tot += ms;
+    }
+    if (total_ms) *total_ms = tot;
+    if (launches) *launches = (uint32_t)(c->kused / 2);
+    if (reset) c->kused = 0;
     return RT_OK;
 }
 
@@ -541,6 +582,28 @@ int rt_set_environment(rt_ctx* c, const float rgb[3])
     return RT_OK;
 }
 
+// Launch the traversal kernel, bracketed by a pair of pooled events when
+// kernel timing is on (rt_kernel_time).
+static int launch_timed(rt_ctx* c, const rtk::DevScene& S, const rtk::DevLaunch& L, rt_mode mode, rt_traverse trav)
+{
+    const bool t = c->ktiming && c->kused + 2 <= 8192;
+    if (t) {
+        while (c->kev.size() < c->kused + 2) {
+            hipEvent_t e;
+            HIPCHK(c, hipEventCreate(&e));
+            c->kev.push_back(e);
+        }
+        HIPCHK(c, hipEventRecord(c->kev[c->kused], c->stream));
+    }
+    int r = rtk::launch_render(S, L, mode, trav, c->detail, c->num_cus, c->waves_per_cu, c->stream);
+    if (r) return fail(c, r, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (t) {
+        HIPCHK(c, hipEventRecord(c->kev[c->kused + 1], c->stream));
+        c->kused += 2;
+    }
+    return RT_OK;
+}
+
 static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
 {
     if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
@@ -589,11 +652,40 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     L.work_counter = c->work.as<uint32_t>();
     L.shade_threshold = (uint32_t)c->shade_threshold;
     L.counters = c->counters.as<unsigned long long>();
-    HIPCHK(c, hipMemsetAsync(c->work.p, 0, 64, c->stream));
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
-    if (L.nwork == 0) return RT_OK;
-    int r = rtk::launch_render(S, L, mode, trav, c->detail, c->num_cus, c->waves_per_cu, c->stream);
-    if (r) return fail(c, r, std::string("kernel launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (L.nwork == 0 || (L.spp == 0 && (mode == RT_MODE_W7E3 || mode == RT_MODE_W9E1))) {
+        if (counts) return rt_last_counts(c, counts);
+        return RT_OK;
+    }
+    if (mode == RT_MODE_W7E3 || mode == RT_MODE_W9E1) {
+        // passes of pass_spp iterations: k_path writes per-iteration samples,
+        // k_fold applies the progressive average in order
+        L.stride = L.tileset ? L.nwork * 64u : L.w * L.h;
+        const uint64_t per_it = (uint64_t)L.stride * sizeof(float4);
+        const uint64_t budget = c->sample_budget_mb << 20;
+        uint32_t pass_spp = (uint32_t)std::min<uint64_t>(L.spp, std::max<uint64_t>(1, budget / per_it));
+        const uint64_t need = per_it * pass_spp;
+        if (c->samples.n < need) HIPCHK(c, c->samples.alloc(need));
+        L.samples = c->samples.as<float4>();
+        const uint32_t first = L.first_iter, total = L.spp;
+        for (uint32_t done = 0; done < total; done += pass_spp) {
+            L.first_iter = first + done;
+            L.spp = std::min(pass_spp, total - done);
+            // work units (chunk, pixel slot) must stay below 2^31: widen chunks if needed
+            uint32_t ch = std::max<uint32_t>(1, std::min(c->sample_chunk, L.spp));
+            while ((uint64_t)L.nwork * 64u * ((L.spp + ch - 1) / ch) >= (1ull << 31)) ch *= 2;
+            L.chunk = ch;
+            L.unit_order = c->unit_order;
+            L.nchunks = (L.spp + ch - 1) / ch;
+            HIPCHK(c, hipMemsetAsync(c->work.p, 0, 64, c->stream));
+            if (int r = launch_timed(c, S, L, mode, trav)) return r;
+            const int r = rtk::launch_fold(L, c->stream);
+            if (r) return fail(c, r, std::string("fold launch failed: ") + hipGetErrorString(hipGetLastError()));
+        }
+    } else {
+        HIPCHK(c, hipMemsetAsync(c->work.p, 0, 64, c->stream));
+        if (int r = launch_timed(c, S, L, mode, trav)) return r;
+    }
     if (counts) return rt_last_counts(c, counts);
     return RT_OK;
 }

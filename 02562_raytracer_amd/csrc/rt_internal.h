@@ -50,8 +50,15 @@ struct DevLaunch {
     uint32_t rank, nranks;
     uint32_t tiles_x, tiles_y;    // tile grid (of the region, or of the frame)
     uint32_t nwork;               // work items (tiles) in this launch
-    uint32_t first_iter, spp;
+    uint32_t first_iter, spp;     // this pass: iterations first_iter .. first_iter+spp-1
     uint32_t shade_threshold;     // k_path: shade when <= this many lanes still trace
+    // k_path work units: (chunk of `chunk` iterations, pixel slot), chunk-major;
+    // per-iteration radiance + primary id go to samples[(it - first_iter) * stride + out]
+    // and k_fold applies the progressive average in order (w7e3.wgsl:261-271)
+    uint32_t chunk, nchunks;
+    uint32_t unit_order;          // 0: chunk-major, 1: pixel-major
+    uint32_t stride;              // output pixels of the launch (region w*h, or nwork*64 packed)
+    float4* samples;
     float4* accum;
     uint32_t* ids;
     uint32_t* work_counter;       // zeroed before launch
@@ -61,6 +68,9 @@ struct DevLaunch {
 // Launch the kernel for (mode, trav); detail = counting instantiation.
 int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traverse trav, bool detail,
                   int num_cus, int waves_per_cu, hipStream_t stream);
+
+// Progressive average of one pass's per-iteration samples into accum/ids (after k_path).
+int launch_fold(const DevLaunch& l, hipStream_t stream);
 
 int launch_unpack(uint32_t width, uint32_t height, uint32_t nranks, uint32_t local_tiles,
                   const float4* packed_accum, const uint32_t* packed_ids, float4* frame_accum,

@@ -275,6 +275,7 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 }
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 as_f4(v4u q)
 {
     return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
@@ -679,7 +680,8 @@ k_path(DevScene S, DevLaunch L)
     const uint32_t light_tris = S.nlights - 1u;
     const uint32_t sel = W9 ? L.u.selection1 : 0u;
     const uint32_t it_end = L.first_iter + L.spp;
-    const uint32_t nslots = L.nwork * 64u;
+    const uint32_t pslots = L.nwork * 64u;            // pixel slots
+    const uint32_t nslots = pslots * L.nchunks;       // work units (host keeps this < 2^31)
     const uint32_t T = L.shade_threshold;
     const f3 env = V(L.env[0], L.env[1], L.env[2]);
     Counters cnt;
@@ -690,8 +692,7 @@ k_path(DevScene S, DevLaunch L)
     enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2 };
     uint32_t st = ST_IDLE;
     bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false;
-    uint32_t px = 0, py = 0, out = 0, it = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
-    float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+    uint32_t px = 0, py = 0, out = 0, it = 0, unit_end = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
     f3 res = V(0, 0, 0), fac = V(1, 1, 1), ro = V(0, 0, 0), rd = V(0, 0, 1), inv = V(0, 0, 0);
     f3 ndir = V(0, 0, 1), cu = V(0, 0, 0), cb = V(0, 0, 0);
     Trav tr;
@@ -842,19 +843,15 @@ k_path(DevScene S, DevLaunch L)
                 }
             }
             if (sample_done) {
-                // accumulation, w7e3.wgsl:261-271
-                const float fi = (float)it, fi1 = (float)(it + 1u);
-                a0 = rt_max0f((res.x + a0 * fi) / fi1);
-                a1 = rt_max0f((res.y + a1 * fi) / fi1);
-                a2 = rt_max0f((res.z + a2 * fi) / fi1);
+                // this iteration's `result` (+ primary id); k_fold accumulates in
+                // iteration order (w7e3.wgsl:261-271).  Streaming store: keep the
+                // scene, not the samples, in L2/MALL.
+                v4f* sp = reinterpret_cast<v4f*>(L.samples + (size_t)(it - L.first_iter) * L.stride + out);
+                const v4f sv = {res.x, res.y, res.z, __uint_as_float(prim)};
+                __builtin_nontemporal_store(sv, sp);
                 it++;
-                if (it < it_end) {
-                    start_sample();
-                } else {
-                    L.accum[out] = make_float4(a0, a1, a2, 1.0f);
-                    if (L.ids) L.ids[out] = prim;
-                    st = ST_IDLE;
-                }
+                if (it < unit_end) start_sample();
+                else st = ST_IDLE;
             }
         }
         // ---- refill idle lanes with new pixels (ballot + mbcnt compaction)
@@ -872,19 +869,24 @@ k_path(DevScene S, DevLaunch L)
                 if (slot >= nslots) {
                     exhausted = true;
                 } else {
-                    const Pix p = map_pixel(L, slot >> 6, slot & 63u);
+                    // chunk-major (unit_order 0): a refill hands out neighbouring
+                    // pixels at the same iteration; pixel-major (1): the iterations
+                    // of one pixel side by side
+                    uint32_t ch, ps;
+                    if (L.unit_order == 0u) {
+                        ch = slot / pslots;
+                        ps = slot - ch * pslots;
+                    } else {
+                        ps = slot / L.nchunks;
+                        ch = slot - ps * L.nchunks;
+                    }
+                    const Pix p = map_pixel(L, ps >> 6, ps & 63u);
                     if (p.valid) {
                         px = p.x;
                         py = p.y;
                         out = p.out;
-                        it = L.first_iter;
-                        a0 = a1 = a2 = 0.0f;
-                        if (L.first_iter > 0u) {
-                            const float4 pa = L.accum[out];
-                            a0 = pa.x;
-                            a1 = pa.y;
-                            a2 = pa.z;
-                        }
+                        it = L.first_iter + ch * L.chunk;
+                        unit_end = it + L.chunk < it_end ? it + L.chunk : it_end;
                         start_sample();
                     }
                 }
@@ -898,6 +900,40 @@ k_path(DevScene S, DevLaunch L)
         if (__ballot(st != ST_IDLE) == 0) break;
     }
     flush_counters(cnt, L.counters, COUNT);
+}
+
+// ------------------------------------------------------------------ progressive fold
+// The accumulation of fs_main (w7e3.wgsl:261-271 / w9e1.wgsl:272-283), applied
+// for iterations first_iter .. first_iter+spp-1 in order to each output pixel:
+// accum = max(vec4((result + prev*it)/(it+1), 1), 0) with prev the stored
+// accumulation (read when first_iter > 0, as the RenderSource texture).  One
+// thread per pixel; samples are [iteration][pixel] so a wave reads 1 KiB
+// contiguous per iteration.  ids = primary hit of the last iteration.
+__global__ void __launch_bounds__(256) k_fold(DevLaunch L)
+{
+    const uint32_t nout = L.tileset ? L.nwork * 64u : L.w * L.h;
+    for (uint32_t o = blockIdx.x * blockDim.x + threadIdx.x; o < nout; o += gridDim.x * blockDim.x) {
+        if (L.tileset && !map_pixel(L, o >> 6, o & 63u).valid) continue;
+        float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+        if (L.first_iter > 0u) {
+            const float4 pa = L.accum[o];
+            a0 = pa.x;
+            a1 = pa.y;
+            a2 = pa.z;
+        }
+        v4f r = {0.0f, 0.0f, 0.0f, 0.0f};
+        const v4f* sp = reinterpret_cast<const v4f*>(L.samples + o);
+        for (uint32_t i = 0; i < L.spp; i++) {
+            r = __builtin_nontemporal_load(sp + (size_t)i * L.stride);
+            const uint32_t it = L.first_iter + i;
+            const float fi = (float)it, fi1 = (float)(it + 1u);
+            a0 = rt_max0f((r.x + a0 * fi) / fi1);
+            a1 = rt_max0f((r.y + a1 * fi) / fi1);
+            a2 = rt_max0f((r.z + a2 * fi) / fi1);
+        }
+        L.accum[o] = make_float4(a0, a1, a2, 1.0f);
+        if (L.ids && L.spp) L.ids[o] = __float_as_uint(r.w);
+    }
 }
 
 // ------------------------------------------------------------------ W6E1 / PROJECT kernel
@@ -1271,6 +1307,16 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
     default:
         return RT_E_UNSUPPORTED;
     }
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+
+int launch_fold(const DevLaunch& l, hipStream_t stream)
+{
+    const uint64_t nout = l.tileset ? (uint64_t)l.nwork * 64u : (uint64_t)l.w * l.h;
+    uint64_t blocks = (nout + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_fold, dim3((uint32_t)blocks), dim3(256), 0, stream, l);
     return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }
 

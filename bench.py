@@ -28,20 +28,21 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+L2_PEAK_GBS = 34500.0   # aggregate L2 (8 XCDs x 4 MiB), MI355X_MICROARCH.md "L2 (per XCD)"
 METRIC = "Mrays/sec primary+shadow at 1920x1080; achieved HBM GB/s vs peak"
 
 
-def algorithmic_bytes(c, trav, npix, first_iter):
+def algorithmic_bytes(c, trav):
     """reference-layout useful bytes of the traversal work,
-    plus the framebuffer bytes one launch moves (accum write, id write, accum
-    read when continuing)."""
+    plus the output bytes k_path writes: one 16-B sample record (radiance +
+    primary id) per pixel-iteration (the fold kernel that averages them is
+    not part of k_path and is timed apart)."""
     if trav == "BSP":
         t = 20 * c["node_interior"] + 16 * c["node_leaf"]
     else:
         t = 32 * c["bvh_pops"]
     t += 4 * c["ids_read"] + 52 * c["tri_tests"] + 36 * c["tri_accepts"]
-    fb = npix * (16 + 4 + (16 if first_iter > 0 else 0))
-    return t + fb
+    return t + 16 * c["samples"]
 
 
 def cpu_baseline(wl, trav, mesh, accel, spp, W, H, budget_s):
@@ -96,6 +97,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--shade-threshold", type=int, default=None)
     ap.add_argument("--waves-per-cu", type=int, default=None)
+    ap.add_argument("--sample-chunk", type=int, default=None)
+    ap.add_argument("--unit-order", type=int, default=None)
     args = ap.parse_args()
 
     import torch
@@ -130,6 +133,10 @@ def main():
         ctx.set_option(rt._ffi.RT_OPT_SHADE_THRESHOLD, args.shade_threshold)
     if args.waves_per_cu is not None:
         ctx.set_option(rt._ffi.RT_OPT_WAVES_PER_CU, args.waves_per_cu)
+    if args.sample_chunk is not None:
+        ctx.set_option(rt._ffi.RT_OPT_SAMPLE_CHUNK, args.sample_chunk)
+    if args.unit_order is not None:
+        ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, args.unit_order)
     ctx.upload_mesh(mesh)
     if trav == "BSP":
         accel = mesh.bsp_tree()
@@ -177,13 +184,17 @@ def main():
         step()
 
     rays = torch.tensor([counts["primary"] + counts["shadow"], counts["primary"], counts["shadow"],
-                         counts["bounce"], algorithmic_bytes(detail, trav, lt * 64, 0)],
+                         counts["bounce"], algorithmic_bytes(detail, trav)],
                         dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(rays)
     rays = rays.cpu().numpy()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # HIP events around each k_path launch, on the stream it runs on (the
+    # step's other kernels -- fold, unpack -- and the gather are excluded)
+    ctx.set_option(rt._ffi.RT_OPT_KERNEL_TIMING, 1)
+    ctx.kernel_time(reset=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -194,17 +205,21 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device=dev)
+    kern_total, launches = ctx.kernel_time(reset=True)
+    ctx.set_option(rt._ffi.RT_OPT_KERNEL_TIMING, 0)
+    launches_per_step = launches // args.steps
+    kern_ms = kern_total / max(1, launches)   # average k_path launch
+    render_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    t = torch.tensor([elapsed, kern_ms, render_ms], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_ms = [float(x) for x in t.cpu().numpy()]
+    elapsed, kern_ms, render_ms = [float(x) for x in t.cpu().numpy()]
 
     value = rays[0] * args.steps / elapsed / 1e6
     if rank == 0:
         # roofline of the dominant kernel (k_path<mode, traversal>): bytes of one launch
         # on one GPU / its average HIP-event duration
-        bytes_per_launch = rays[4] / world
+        bytes_per_launch = rays[4] / world / max(1, launches_per_step)
         achieved = bytes_per_launch / (kern_ms / 1e3) / 1e9
         traffic = None
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -227,7 +242,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": f"k_path<{wl.mode},{trav}>", "kernel_ms": round(kern_ms, 3),
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch)},
+                         "launches_per_step": launches_per_step, "render_ms": round(render_ms, 3),
+                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
+                         # the scene is cache-resident: the same bytes against the chip's
+                         # aggregate L2 bandwidth (MI355X_MICROARCH.md: ~34.5 TB/s)
+                         "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
             "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},
             "traversal_per_launch": {k: detail[k] for k in ("node_interior", "node_leaf", "bvh_pops", "tri_tests",

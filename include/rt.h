@@ -151,7 +151,12 @@ typedef struct rt_ray_counts {
 /* ---- options (rt_set_option) ------------------------------------------- */
 #define RT_OPT_DETAIL_COUNTERS 1  /* 0/1: use the counting kernel instantiation    */
 #define RT_OPT_WAVES_PER_CU    2  /* persistent grid size: waves per CU (default 20) */
-#define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace; 64 = all lanes finish their rays first (lockstep) */
+#define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace (default 8); 0 or 64 = all lanes finish their rays first (lockstep) */
+#define RT_OPT_SAMPLE_CHUNK    4  /* W7E3/W9E1: progressive iterations per work unit (default 1) */
+#define RT_OPT_SAMPLE_BUDGET_MB 5 /* W7E3/W9E1: device scratch for per-sample results, MiB (default 16384);
+                                     a render whose spp x pixels x 16 B exceed it runs in several passes */
+#define RT_OPT_KERNEL_TIMING   7  /* 0/1: record HIP events around every traversal-kernel launch */
+#define RT_OPT_UNIT_ORDER      6  /* W7E3/W9E1 work-unit order: 0 chunk-major, 1 pixel-major (default) */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
 
@@ -190,6 +195,13 @@ int rt_memset_device(rt_ctx* ctx, void* dst_dev, int value, size_t bytes);
  * times render() on the host; this times the device work). */
 int rt_timer_start(rt_ctx* ctx);
 int rt_timer_stop(rt_ctx* ctx, float* ms);   /* synchronizes */
+
+/* Per-launch timing of the traversal kernels (k_path / k_primary / k_w1e6),
+ * enabled by RT_OPT_KERNEL_TIMING: HIP events around every such launch on the
+ * context stream.  rt_kernel_time synchronizes and returns the summed
+ * duration and the number of launches since the last reset (reset != 0
+ * clears them).  At most 4096 launches are kept between resets. */
+int rt_kernel_time(rt_ctx* ctx, int reset, double* total_ms, uint32_t* launches);
 
 /* ---- uploads (replace the src/bindings/ create_buffer_init calls) ------------- */
 
@@ -231,6 +243,11 @@ int rt_set_environment(rt_ctx* ctx, const float rgb[3]);
 
 /* Trace `spp` progressive iterations first_iter .. first_iter+spp-1 for every
  * pixel of `region` (global pixel coordinates inside uniforms.resolution).
+ * W7E3/W9E1 split the iterations of a pixel into work units of
+ * RT_OPT_SAMPLE_CHUNK iterations that run in parallel; each unit writes its
+ * per-iteration radiance to device scratch, and a fold kernel then applies the
+ * reference's progressive average in iteration order (bit-identical to
+ * `spp` sequential render() calls).
  *   accum_rgba32f: DEVICE, region.w*region.h float4, row-major over the region,
  *     in/out: holds the accumulation of iterations < first_iter (read when
  *     first_iter > 0; the RenderDestination texture, render_state.rs:541-555),

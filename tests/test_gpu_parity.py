@@ -67,6 +67,28 @@ def test_cornell_w7e3_progressive_continuation(cornell_bsp):
     check(b, o)
 
 
+@pytest.mark.parametrize("chunk,order,budget_mb", [(1, 1, None), (3, 0, None), (1, 0, 1), (5, 1, 1), (64, 1, None)])
+def test_work_units_and_passes(rt, cornell_bsp, chunk, order, budget_mb):
+    # k_path work units of `chunk` iterations in either order, and renders split
+    # into passes by the per-sample scratch budget (1 MiB = 10 iterations of
+    # 160x160 px): the progressive fold reproduces the in-order accumulation bit
+    # for bit, for any unit shape (regions with ragged 8x8 tiles)
+    s = cornell_bsp
+    try:
+        s.ctx.set_option(rt._ffi.RT_OPT_SAMPLE_CHUNK, chunk)
+        s.ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, order)
+        if budget_mb:
+            s.ctx.set_option(rt._ffi.RT_OPT_SAMPLE_BUDGET_MB, budget_mb)
+        accum_in = s.render_gpu("W7E3", CORNELL_CAM, 200, 180, (20, 10, 160, 160), 0, 3)[0]
+        g = s.render_gpu("W7E3", CORNELL_CAM, 200, 180, (20, 10, 160, 160), 3, 13, accum_in=accum_in)
+        o = s.render_oracle("W7E3", CORNELL_CAM, 200, 180, (20, 10, 160, 160), 3, 13, accum_in=accum_in.copy())
+    finally:
+        s.ctx.set_option(rt._ffi.RT_OPT_SAMPLE_CHUNK, 1)
+        s.ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, 1)
+        s.ctx.set_option(rt._ffi.RT_OPT_SAMPLE_BUDGET_MB, 16384)
+    check(g, o)
+
+
 def test_cornell_w7e3_bvh(rt, gpu):
     s = Scene(rt, rt.Mesh.from_obj(model("CornellBoxWithBlocks.obj")), "BVH")
     g = s.render_gpu("W7E3", CORNELL_CAM, 64, 64, (0, 0, 64, 64), 0, 2)
