@@ -54,7 +54,7 @@ struct rt_ctx {
     hipStream_t stream = nullptr;
     std::string err;
     int num_cus = 256;
-    int waves_per_cu = 20;   // 5 waves per SIMD: the k_path register budget (RT_PATH_WAVES_PER_EU)
+    int waves_per_cu = 32;   // 8 waves per SIMD: the k_path register budget (RT_PATH_WAVES_PER_EU)
     int shade_threshold = 8;    // with pixel-major units: lanes refill together (coherent samples)
     uint32_t sample_chunk = 1;          // iterations per k_path work unit
     uint32_t unit_order = 1;            // 0: chunk-major, 1: pixel-major
