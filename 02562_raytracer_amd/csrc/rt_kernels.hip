@@ -165,18 +165,13 @@ __device__ __forceinline__ void pixel_uv(const rt_uniform& u, uint32_t x, uint32
 // Exact fast rejection: the accept predicate is a pure function of the
 // correctly rounded quotients beta = a/denom, gamma = b/denom, dist = c/denom,
 // so a quotient is only divided out when its sign/range is not already
-// certain.  RN(a/denom) < 0  <=>  a != 0, sign(a) != sign(denom) and the
-// quotient does not underflow to -0; with 2^-60 <= |a| and |denom| <= 2^60
-// the quotient is >= 2^-120 in magnitude, far from the 2^-150 underflow
-// threshold, so the sign test is exact there (anything else falls back to
-// the division).  The dist range test uses v_rcp_f32 (<= 1 ulp) with a
-// 2^-20 relative margin, which bounds |RN(c*rcp(denom)) - RN(c/denom)|.
-__device__ __forceinline__ bool sign_certain_neg(float a, float den)
-{
-    return (a != 0.0f) & (rt_absf(a) >= 0x1p-60f) & (((__float_as_uint(a) ^ __float_as_uint(den)) >> 31) != 0u);
-}
-__device__ __forceinline__ bool sign_uncertain(float a) { return a != 0.0f && !(rt_absf(a) >= 0x1p-60f); }
-
+// certain.  With 1e-10 <= |denom| <= 2^60, r = v_rcp_f32(denom) is a normal
+// number within 1 ulp of 1/denom, so a*r carries the quotient's sign and is
+// within 2^-22 relative of it: a*r < -2^-100 makes a/denom a negative number of
+// magnitude > 2^-101, far from the 2^-150 underflow threshold, so RN(a/denom) < 0
+// (an infinite a*r means an infinite quotient of the same sign; NaN compares
+// false and falls back to the division).  The dist range test uses the same r
+// with a 2^-20 relative margin, which bounds |RN(c*r) - RN(c/denom)|.
 template <bool FAST, bool COUNT = false>
 __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const float4 r2, f3 o, f3 w, float tmin,
                                          float tmax, float& dist, float& beta, float& gamma, Counters* cn = nullptr)
@@ -196,10 +191,10 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
         // RN(beta + gamma) > 1 (needs beta + gamma > 1 + 2^-24: margin 2^-22)
         const float r = __builtin_amdgcn_rcpf(denom);
         const float tq = c * r;
-        const float m = rt_absf(tq) * 0x1p-20f + 1e-30f;
+        const float m = __builtin_fmaf(rt_absf(tq), 0x1p-20f, 1e-30f);   // the product is exact: = mul + add
         const float qa = a * r, qb = b * r;
         const float ms = (rt_absf(qa) + rt_absf(qb)) * 0x1p-20f;
-        reject = reject | ((rt_absf(denom) <= 0x1p60f) & (sign_certain_neg(a, denom) | sign_certain_neg(b, denom) |
+        reject = reject | ((rt_absf(denom) <= 0x1p60f) & ((qa < -0x1p-100f) | (qb < -0x1p-100f) |
                                                           (tq - m > tmax) | (tq + m < tmin) |
                                                           (qa + qb - ms > 1.0f + 0x1p-22f)));
     }
@@ -299,7 +294,7 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     const uint32_t near_node = 2u * m + (__float_as_uint(iv) >> 31);   // see bsp_inv1
     const float x = __uint_as_float(n.y) - ao;
     const float tq = x * iv;
-    const float mg = rt_absf(tq) * 0x1p-20f + 1e-30f;
+    const float mg = __builtin_fmaf(rt_absf(tq), 0x1p-20f, 1e-30f);   // exact product: = mul + add
     // (bitwise & | on bools: no short-circuit control flow)
     const bool cnear = tq - mg > t.tmax;                                   // certainly t > tmax
     const bool cfar = (!cnear) & (tq + mg < t.tmin) & (tq + mg <= t.tmax);   // certainly !(t > tmax) && t < tmin
@@ -688,6 +683,7 @@ k_path(DevScene S, DevLaunch L)
     const uint32_t pslots = L.nwork * 64u;            // pixel slots
     const uint32_t nslots = pslots * L.nchunks;       // work units (host keeps this < 2^31)
     const uint32_t T = L.shade_threshold;
+    const uint32_t KH = L.min_half_lanes;
     const f3 env = V(L.env[0], L.env[1], L.env[2]);
     Counters cnt;
 #pragma unroll
@@ -749,7 +745,18 @@ k_path(DevScene S, DevLaunch L)
                     cnt.v[C_LEAF_TRIPS] += lm != 0;
                 }
             }
-            if (st == ST_TRACE) {
+            bool go = st == ST_TRACE;
+            if (KH > 0u) {
+                // postpone the minority half of a divergent trip: lanes inside a
+                // leaf (triangle test) and walking lanes (node steps) run the two
+                // halves of bsp_step/bvh_step; a half with fewer than KH lanes
+                // waits while the other half has at least KH
+                const bool leafst = tr.leaf_k != tr.leaf_end;
+                const uint32_t nl = (uint32_t)__popcll(__ballot(go && leafst));
+                const uint32_t nn = (uint32_t)__popcll(__ballot(go && !leafst));
+                go = go && (leafst ? (nl >= KH || nn < KH) : (nn >= KH || nl < KH));
+            }
+            if (go) {
                 if (trav_step<TRAV, COUNT>(S, stk, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }
         }
