@@ -52,6 +52,16 @@ class GpuNode(C.Structure):           # src/data_structures/hlbvh.rs:508-515
                 ("n_prims", C.c_uint32)]
 
 
+class BvhBuildTimes(C.Structure):    # include/rt.h rt_bvh_build_times (bvh_util.rs BvhConstructionTime)
+    _fields_ = [(n, C.c_double) for n in ("morton_codes_ms", "radix_sort_ms", "treelet_init_ms",
+                                          "treelet_build_ms", "upper_tree_ms", "upper_tree_host_ms",
+                                          "flattening_ms", "total_ms")] + [("treelets", C.c_uint32),
+                                                                            ("nodes", C.c_uint32)]
+
+    def asdict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 class Uniform(C.Structure):           # src/bindings/uniform.rs:6-34
     _fields_ = [("camera_pos", C.c_float * 3), ("camera_constant", C.c_float),
                 ("camera_look_at", C.c_float * 3), ("aspect_ratio", C.c_float),
@@ -114,6 +124,8 @@ SIGNATURES = {
     "rt_timer_start": (C.c_int, [vp]),
     "rt_timer_stop": (C.c_int, [vp, f32p]),
     "rt_kernel_time": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), u32p]),
+    "rt_build_bvh_device": (C.c_int, [vp, C.c_uint32, C.POINTER(BvhBuildTimes)]),
+    "rt_download_bvh": (C.c_int, [vp, C.POINTER(GpuNode), C.c_uint32, u32p, C.c_uint32, u32p, u32p]),
     "rt_upload_mesh": (C.c_int, [vp, f32p, f32p, C.c_uint32, u32p, C.c_uint32, C.POINTER(Material), C.c_uint32,
                                  u32p, C.c_uint32]),
     "rt_upload_bsp": (C.c_int, [vp, f32p, u32p, f32p, C.c_uint32, u32p, C.c_uint32, C.c_uint32]),

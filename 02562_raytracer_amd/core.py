@@ -265,6 +265,25 @@ class Context:
     def upload_bvh(self, bvh):
         self._chk(F.lib().rt_upload_bvh_host(self._h, bvh.handle))
 
+    def build_bvh_device(self, max_prims=4):
+        """HLBVH construction on the device from the uploaded mesh
+        (hlbvh::Bvh::new + flatten + triangles, rt_build_bvh_device); becomes
+        this context's BVH.  Returns the per-phase times (ms)."""
+        t = F.BvhBuildTimes()
+        self._chk(F.lib().rt_build_bvh_device(self._h, max_prims, C.byref(t)))
+        return t.asdict()
+
+    def download_bvh(self):
+        """(nodes[n,8] u32 view of GpuNode, tri_ids[k] u32) of this context's BVH."""
+        nn, ni = C.c_uint32(), C.c_uint32()
+        self._chk(F.lib().rt_download_bvh(self._h, None, 0, None, 0, C.byref(nn), C.byref(ni)))
+        nodes = (F.GpuNode * max(1, nn.value))()
+        ids = np.zeros(max(1, ni.value), np.uint32)
+        self._chk(F.lib().rt_download_bvh(self._h, nodes, nn.value, ids.ctypes.data_as(F.u32p), ni.value,
+                                          C.byref(nn), C.byref(ni)))
+        raw = np.frombuffer(nodes, dtype=np.uint32).reshape(-1, 8)[:nn.value].copy()
+        return raw, ids[:ni.value].copy()
+
     def upload_mesh_arrays(self, vertices, normals, indices, materials, lights=None):
         pos = np.ascontiguousarray(vertices, dtype=np.float32).reshape(-1, 4)
         nrm = np.ascontiguousarray(normals, dtype=np.float32).reshape(-1, 4)

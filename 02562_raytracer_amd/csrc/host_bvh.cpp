@@ -120,34 +120,57 @@ struct Lbvh {
     }
 };
 
-bool center_less(const BNode* a, const BNode* b, int dim)   // f32::total_cmp on the centroid
+bool center_less(const Box& a, const Box& b, int dim)   // f32::total_cmp on the centroid
 {
-    const float ca = (a->bbox.mn[dim] + a->bbox.mx[dim]) * 0.5f, cb = (b->bbox.mn[dim] + b->bbox.mx[dim]) * 0.5f;
+    const float ca = (a.mn[dim] + a.mx[dim]) * 0.5f, cb = (b.mn[dim] + b.mx[dim]) * 0.5f;
     if (ca < cb) return true;
     if (ca > cb) return false;
     return signbit(ca) && !signbit(cb);
 }
 
-std::unique_ptr<BNode> collapse(std::vector<std::unique_ptr<BNode>>& nodes, size_t lo, size_t hi, uint32_t& total)
-{   // collapse_build_nodes_recursive + mid_partition, :252-291
+// collapse_build_nodes_recursive + mid_partition (:252-291) over entry indices
+// ids[lo, hi); returns the entry index of the subtree root.
+int32_t collapse(std::vector<rthost::UpperNode>& e, std::vector<int32_t>& ids, size_t lo, size_t hi, uint32_t& total)
+{
     const size_t n = hi - lo;
-    if (n == 1) return std::move(nodes[lo]);
+    if (n == 1) return ids[lo];
     total++;
     Box cb = box_new();
     for (size_t i = lo; i < hi; i++) {
+        const Box bx{{e[ids[i]].mn[0], e[ids[i]].mn[1], e[ids[i]].mn[2]}, {e[ids[i]].mx[0], e[ids[i]].mx[1], e[ids[i]].mx[2]}};
         float c[3];
-        center(nodes[i]->bbox, c);
+        center(bx, c);
         include_v(cb, c);
     }
     const float d0 = cb.mx[0] - cb.mn[0], d1 = cb.mx[1] - cb.mn[1], d2 = cb.mx[2] - cb.mn[2];
     const int dim = d0 > d1 ? (d0 > d2 ? 0 : 2) : (d1 > d2 ? 1 : 2);   // longest_axis, bbox.rs:128-143
-    std::stable_sort(nodes.begin() + lo, nodes.begin() + hi,
-                     [dim](const std::unique_ptr<BNode>& a, const std::unique_ptr<BNode>& b) {
-                         return center_less(a.get(), b.get(), dim);
-                     });
+    std::stable_sort(ids.begin() + lo, ids.begin() + hi, [&e, dim](int32_t a, int32_t b) {
+        const Box ba{{e[a].mn[0], e[a].mn[1], e[a].mn[2]}, {e[a].mx[0], e[a].mx[1], e[a].mx[2]}};
+        const Box bb{{e[b].mn[0], e[b].mn[1], e[b].mn[2]}, {e[b].mx[0], e[b].mx[1], e[b].mx[2]}};
+        return center_less(ba, bb, dim);
+    });
     const size_t mid = lo + n / 2;
-    auto a = collapse(nodes, lo, mid, total);
-    auto b = collapse(nodes, mid, hi, total);
+    const int32_t a = collapse(e, ids, lo, mid, total);
+    const int32_t b = collapse(e, ids, mid, hi, total);
+    rthost::UpperNode x;   // BvhBuildNode::new_internal: bbox = child0's, include child1's
+    for (int i = 0; i < 3; i++) {
+        x.mn[i] = rt_minf(e[a].mn[i], e[b].mn[i]);
+        x.mx[i] = rt_maxf(e[a].mx[i], e[b].mx[i]);
+    }
+    x.root = -1;
+    x.left = a;
+    x.right = b;
+    e.push_back(x);
+    return (int32_t)e.size() - 1;
+}
+
+// the root's subtree, rebuilt as BNodes from the upper-tree entries
+std::unique_ptr<BNode> to_bnodes(const std::vector<rthost::UpperNode>& e, int32_t i,
+                                 std::vector<std::unique_ptr<BNode>>& roots)
+{
+    if (e[i].root >= 0) return std::move(roots[e[i].root]);
+    auto a = to_bnodes(e, e[i].left, roots);
+    auto b = to_bnodes(e, e[i].right, roots);
     return make_internal(std::move(a), std::move(b));
 }
 
@@ -178,6 +201,10 @@ extern "C" int rt_bvh_build(const rt_mesh_host* mesh, uint32_t max_prims, rt_bvh
 {
     if (!mesh || !out || mesh->ntris() == 0) {
         rthost::set_error("rt_bvh_build: empty mesh");
+        return RT_E_INVALID;
+    }
+    if (max_prims == 0) {   // emit_lbvh would read morton_primitives[offset - 1] for an empty range
+        rthost::set_error("rt_bvh_build: max_prims must be >= 1");
         return RT_E_INVALID;
     }
     const uint32_t nt = mesh->ntris();
@@ -235,7 +262,15 @@ extern "C" int rt_bvh_build(const rt_mesh_host* mesh, uint32_t max_prims, rt_bvh
     for (auto& t : th) t.join();
     uint32_t total = 0;
     for (uint32_t c : counts) total += c;
-    auto root = collapse(roots, 0, roots.size(), total);
+    std::vector<float> rb(roots.size() * 6);
+    for (size_t i = 0; i < roots.size(); i++)
+        for (int k = 0; k < 3; k++) {
+            rb[i * 6 + k] = roots[i]->bbox.mn[k];
+            rb[i * 6 + 3 + k] = roots[i]->bbox.mx[k];
+        }
+    std::vector<rthost::UpperNode> upper;
+    total += rthost::bvh_upper_tree(rb, upper);
+    auto root = to_bnodes(upper, 0, roots);
     rt_bvh_host* b = new rt_bvh_host();
     rt_gpu_node filler;   // GpuNode::new(root bbox), :518-525
     for (int i = 0; i < 3; i++) {
@@ -251,6 +286,37 @@ extern "C" int rt_bvh_build(const rt_mesh_host* mesh, uint32_t max_prims, rt_bvh
     for (uint32_t k = 0; k < nt; k++) b->tri_ids[k] = mp[k].index;
     *out = b;
     return RT_OK;
+}
+
+uint32_t rthost::bvh_upper_tree(const std::vector<float>& root_boxes, std::vector<UpperNode>& out)
+{
+    const size_t n = root_boxes.size() / 6;
+    out.clear();
+    out.reserve(2 * n);
+    std::vector<int32_t> ids(n);
+    for (size_t i = 0; i < n; i++) {
+        UpperNode x;
+        for (int k = 0; k < 3; k++) {
+            x.mn[k] = root_boxes[i * 6 + k];
+            x.mx[k] = root_boxes[i * 6 + 3 + k];
+        }
+        x.root = (int32_t)i;
+        x.left = x.right = -1;
+        out.push_back(x);
+        ids[i] = (int32_t)i;
+    }
+    uint32_t total = 0;
+    if (n == 0) return 0;
+    const int32_t r = collapse(out, ids, 0, n, total);
+    // put the root first: entry 0 <-> r
+    if (r != 0) {
+        std::swap(out[0], out[(size_t)r]);
+        for (auto& x : out) {
+            if (x.left == 0) x.left = r; else if (x.left == r) x.left = 0;
+            if (x.right == 0) x.right = r; else if (x.right == r) x.right = 0;
+        }
+    }
+    return total;
 }
 
 extern "C" int rt_bvh_view_get(const rt_bvh_host* b, rt_bvh_view* v)

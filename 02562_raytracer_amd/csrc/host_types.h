@@ -34,6 +34,18 @@ namespace rthost {
 // StorageMeshGpu light list (src/bindings/storage_mesh.rs:316-326).
 std::vector<uint32_t> light_list(const std::vector<uint32_t>& idx, const std::vector<rt_material>& mats);
 rt_material default_material();
+// hlbvh.rs upper tree (collapse_build_nodes_recursive + mid_partition,
+// src/data_structures/hlbvh.rs:252-291) over the treelet roots' boxes
+// (mn.xyz, mx.xyz each): nodes[0] is the root when there are >= 2 roots.
+// An entry with root >= 0 stands for treelet root `root`; otherwise it is an
+// internal node whose children are entries `left` and `right` (child0 first).
+// Returns the number of internal nodes (the `total_nodes` increments).
+struct UpperNode {
+    float mn[3], mx[3];
+    int32_t root;          // treelet index, or -1 for an internal node
+    int32_t left, right;   // entry indices (internal nodes)
+};
+uint32_t bvh_upper_tree(const std::vector<float>& root_boxes, std::vector<UpperNode>& out);
 // thread-local last error for context-less calls
 void set_error(const std::string& msg);
 const char* get_error();

@@ -39,6 +39,12 @@ struct DevBuf {
         n = bytes;
         return hipSuccess;
     }
+    void adopt(void* q, size_t bytes)   // take ownership of a hipMalloc'ed block
+    {
+        reset();
+        p = q;
+        n = bytes;
+    }
     template <class T>
     T* as() const
     {
@@ -74,8 +80,9 @@ struct rt_ctx {
     float aabb[6] = {0, 0, 0, 0, 0, 0};
     bool has_bsp = false;
     DevBuf bvh_nodes, bvh_ids;   // bvh_nodes: [32-B nodes | 48-B records]
+    DevBuf bvh_ref;              // the GpuNode array in the reference layout (rt_download_bvh)
     uint32_t bvh_rec_off = 0;
-    uint32_t bvh_nnodes = 0;
+    uint32_t bvh_nnodes = 0, bvh_nids = 0;
     bool has_bvh = false;
     rt_uniform u;
     bool has_u = false;
@@ -554,8 +561,68 @@ int rt_upload_bvh(rt_ctx* c, const rt_gpu_node* nodes, uint32_t nnodes, const ui
     }
     c->bvh_rec_off = (uint32_t)rec_off;
     if ((r = upload(c, c->bvh_ids, tri_ids, (size_t)nids * 4))) return r;
+    if ((r = upload(c, c->bvh_ref, nodes, (size_t)nnodes * sizeof(rt_gpu_node)))) return r;
     c->bvh_nnodes = nnodes;
+    c->bvh_nids = nids;
     c->has_bvh = true;
+    return RT_OK;
+}
+
+int rt_build_bvh_device(rt_ctx* c, uint32_t max_prims, rt_bvh_build_times* times)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_build_bvh_device: upload the mesh first");
+    if (max_prims == 0) return fail(c, RT_E_INVALID, "rt_build_bvh_device: max_prims must be >= 1");
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_bvh = false;
+    rtk::BvhDeviceOut o;
+    std::string err;
+    const int r = rtk::build_bvh_device(c->pos.as<float4>(), c->idx.as<uint4>(), c->ntris, max_prims, c->num_cus,
+                                        c->stream, o, times, err);
+    DevBuf nodes_ref, ids;   // own the outputs from here on
+    if (o.nodes) nodes_ref.adopt(o.nodes, (size_t)o.nnodes * sizeof(rt_gpu_node));
+    if (o.ids) ids.adopt(o.ids, (size_t)o.nids * 4);
+    if (r) return fail(c, r, err);
+    // traversal layout, as rt_upload_bvh (records of the bvh_triangles slots)
+    const size_t rec_off = ((size_t)o.nnodes * 32 + 255) & ~(size_t)255;
+    const size_t total = rec_off + (size_t)o.nids * 48;
+    if (total >= ((size_t)1 << 32))
+        return fail(c, RT_E_UNSUPPORTED, "rt_build_bvh_device: BVH nodes + records must stay below 4 GiB");
+    HIPCHK(c, c->bvh_nodes.alloc(total));
+    if (rtk::launch_bvh_repack(nodes_ref.as<rt_gpu_node>(), o.nnodes, (uint32_t)rec_off, c->bvh_nodes.p,
+                               c->pos.as<float4>(), c->idx.as<uint4>(), ids.as<uint32_t>(), o.nids, c->stream))
+        return fail(c, RT_E_DEVICE, "rt_build_bvh_device: repack launch failed");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->bvh_ref.adopt(nodes_ref.p, nodes_ref.n);
+    nodes_ref.p = nullptr;
+    c->bvh_ids.adopt(ids.p, ids.n);
+    ids.p = nullptr;
+    c->bvh_rec_off = (uint32_t)rec_off;
+    c->bvh_nnodes = o.nnodes;
+    c->bvh_nids = o.nids;
+    c->has_bvh = true;
+    return RT_OK;
+}
+
+int rt_download_bvh(rt_ctx* c, rt_gpu_node* nodes, uint32_t cap_nodes, uint32_t* tri_ids, uint32_t cap_ids,
+                    uint32_t* nnodes, uint32_t* nids)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->has_bvh) return fail(c, RT_E_NOT_READY, "rt_download_bvh: no BVH on the context");
+    if (nnodes) *nnodes = c->bvh_nnodes;
+    if (nids) *nids = c->bvh_nids;
+    if (int r = set_dev(c)) return r;
+    if (nodes) {
+        if (cap_nodes < c->bvh_nnodes) return fail(c, RT_E_INVALID, "rt_download_bvh: node array too small");
+        HIPCHK(c, hipMemcpyAsync(nodes, c->bvh_ref.p, (size_t)c->bvh_nnodes * sizeof(rt_gpu_node),
+                                 hipMemcpyDeviceToHost, c->stream));
+    }
+    if (tri_ids) {
+        if (cap_ids < c->bvh_nids) return fail(c, RT_E_INVALID, "rt_download_bvh: id array too small");
+        HIPCHK(c, hipMemcpyAsync(tri_ids, c->bvh_ids.p, (size_t)c->bvh_nids * 4, hipMemcpyDeviceToHost, c->stream));
+    }
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return RT_OK;
 }
 

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "../../include/rt.h"
 
 namespace rtk {
@@ -76,6 +78,19 @@ int launch_fold(const DevLaunch& l, hipStream_t stream);
 int launch_unpack(uint32_t width, uint32_t height, uint32_t nranks, uint32_t local_tiles,
                   const float4* packed_accum, const uint32_t* packed_ids, float4* frame_accum,
                   uint32_t* frame_ids, hipStream_t stream);
+
+// GPU HLBVH build (rt_build.hip): reference-layout arrays (GpuNode + bvh_triangles),
+// device allocations owned by the caller afterwards (hipFree).
+struct BvhDeviceOut {
+    rt_gpu_node* nodes = nullptr;
+    uint32_t* ids = nullptr;
+    uint32_t nnodes = 0, nids = 0;
+};
+int build_bvh_device(const float4* pos, const uint4* idx, uint32_t ntris, uint32_t max_prims, int num_cus,
+                     hipStream_t stream, BvhDeviceOut& out, rt_bvh_build_times* times, std::string& err);
+// traversal layout of a BVH from its reference-layout arrays (rt_upload_bvh's repack, on device)
+int launch_bvh_repack(const rt_gpu_node* nodes, uint32_t nnodes, uint32_t rec_off, void* blob, const float4* pos,
+                      const uint4* idx, const uint32_t* ids, uint32_t nids, hipStream_t stream);
 
 int launch_selftest_math(const float* in, float* out, uint32_t n, hipStream_t stream);
 

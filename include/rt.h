@@ -236,6 +236,32 @@ int rt_upload_bvh(rt_ctx* ctx, const rt_gpu_node* nodes, uint32_t nnodes,
  * compute_jitters returns (0,0), uniform.rs:261-263). */
 int rt_set_uniforms(rt_ctx* ctx, const rt_uniform* u, const float* jitter);
 
+/* ---- acceleration-structure construction on the GPU ---- */
+
+/* Per-phase times of a device build, the reference's BvhConstructionTime
+ * split (src/data_structures/bvh_util.rs:6-13, src/bin/bvh_project.rs). */
+typedef struct rt_bvh_build_times {
+    double morton_codes_ms, radix_sort_ms, treelet_init_ms, treelet_build_ms;
+    double upper_tree_ms;        /* device-to-host of the treelet roots + host collapse + upload */
+    double upper_tree_host_ms;   /* of which the host collapse                                    */
+    double flattening_ms;        /* DFS offsets, GpuNode array, filler                            */
+    double total_ms;             /* wall clock of the whole call                                  */
+    uint32_t treelets, nodes;
+} rt_bvh_build_times;
+
+/* hlbvh::Bvh::new(mesh, max_prims) + flatten() + triangles()
+ * (src/data_structures/hlbvh.rs:36-239) on the device from the context's
+ * uploaded mesh: the same arrays as rt_bvh_build (equal Morton codes in
+ * primitive-index order), installed as the context's BVH as rt_upload_bvh
+ * would.  times may be NULL.  Synchronizes the context stream. */
+int rt_build_bvh_device(rt_ctx* ctx, uint32_t max_prims, rt_bvh_build_times* times);
+
+/* Copy the context's BVH in the reference layout (GpuNode array, bvh_triangles)
+ * to host arrays of capacity cap_nodes / cap_ids; the sizes are stored in
+ * nnodes / nids (pass NULL arrays to query them). */
+int rt_download_bvh(rt_ctx* ctx, rt_gpu_node* nodes, uint32_t cap_nodes, uint32_t* tri_ids, uint32_t cap_ids,
+                    uint32_t* nnodes, uint32_t* nids);
+
 /* Environment radiance returned on escape by RT_MODE_W9E1 (stands in for the
  * equirectangular hdri0 texture, res/shaders/w9e1.wgsl:232-241). Default (1,1,1). */
 int rt_set_environment(rt_ctx* ctx, const float rgb[3]);
