@@ -62,6 +62,14 @@ class BvhBuildTimes(C.Structure):    # include/rt.h rt_bvh_build_times (bvh_util
         return {n: getattr(self, n) for n, _ in self._fields_}
 
 
+class BspBuildTimes(C.Structure):    # include/rt.h rt_bsp_build_times
+    _fields_ = [("subdivision_ms", C.c_double), ("flattening_ms", C.c_double), ("total_ms", C.c_double),
+                ("levels", C.c_uint32), ("leaves", C.c_uint32), ("nids", C.c_uint32)]
+
+    def asdict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
 class Uniform(C.Structure):           # src/bindings/uniform.rs:6-34
     _fields_ = [("camera_pos", C.c_float * 3), ("camera_constant", C.c_float),
                 ("camera_look_at", C.c_float * 3), ("aspect_ratio", C.c_float),
@@ -125,6 +133,8 @@ SIGNATURES = {
     "rt_timer_stop": (C.c_int, [vp, f32p]),
     "rt_kernel_time": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), u32p]),
     "rt_build_bvh_device": (C.c_int, [vp, C.c_uint32, C.POINTER(BvhBuildTimes)]),
+    "rt_build_bsp_device": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(BspBuildTimes)]),
+    "rt_download_bsp": (C.c_int, [vp, u32p, f32p, C.c_uint32, u32p, C.c_uint32, f32p, u32p, u32p]),
     "rt_download_bvh": (C.c_int, [vp, C.POINTER(GpuNode), C.c_uint32, u32p, C.c_uint32, u32p, u32p]),
     "rt_upload_mesh": (C.c_int, [vp, f32p, f32p, C.c_uint32, u32p, C.c_uint32, C.POINTER(Material), C.c_uint32,
                                  u32p, C.c_uint32]),

@@ -273,6 +273,27 @@ class Context:
         self._chk(F.lib().rt_build_bvh_device(self._h, max_prims, C.byref(t)))
         return t.asdict()
 
+    def build_bsp_device(self, max_depth=20, max_leaf=4):
+        """BSP construction on the device from the uploaded mesh
+        (BspTree::new + bsp_array + primitive_ids, rt_build_bsp_device);
+        becomes this context's BSP.  Returns the phase times (ms)."""
+        t = F.BspBuildTimes()
+        self._chk(F.lib().rt_build_bsp_device(self._h, max_depth, max_leaf, C.byref(t)))
+        return t.asdict()
+
+    def download_bsp(self):
+        """(tree[n,4] u32, planes[n] f32, ids[k] u32, aabb[8] f32) of this context's BSP."""
+        nn, ni = C.c_uint32(), C.c_uint32()
+        self._chk(F.lib().rt_download_bsp(self._h, None, None, 0, None, 0, None, C.byref(nn), C.byref(ni)))
+        tree = np.zeros((max(1, nn.value), 4), np.uint32)
+        planes = np.zeros(max(1, nn.value), np.float32)
+        ids = np.zeros(max(1, ni.value), np.uint32)
+        aabb = np.zeros(8, np.float32)
+        self._chk(F.lib().rt_download_bsp(self._h, tree.ctypes.data_as(F.u32p), planes.ctypes.data_as(F.f32p),
+                                          nn.value, ids.ctypes.data_as(F.u32p), ni.value,
+                                          aabb.ctypes.data_as(F.f32p), C.byref(nn), C.byref(ni)))
+        return tree[:nn.value], planes[:nn.value], ids[:ni.value], aabb
+
     def download_bvh(self):
         """(nodes[n,8] u32 view of GpuNode, tri_ids[k] u32) of this context's BVH."""
         nn, ni = C.c_uint32(), C.c_uint32()

@@ -75,6 +75,9 @@ struct rt_ctx {
     bool has_mesh = false;
     DevBuf pos, nrm, idx, mats, lights;
     DevBuf bsp_nodes, bsp_ids;   // bsp_nodes: [8-B nodes | 48-B records]
+    DevBuf bsp_ref_tree, bsp_ref_planes;   // bsp_array + planes in the reference layout (rt_download_bsp)
+    float bsp_aabb8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t bsp_nnodes = 0, bsp_nids = 0;
     uint32_t bsp_rec_off = 0;
     uint32_t bsp_depth = 0;
     float aabb[6] = {0, 0, 0, 0, 0, 0};
@@ -491,6 +494,11 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
     }
     c->bsp_rec_off = (uint32_t)rec_off;
     if ((r = upload(c, c->bsp_ids, ids, (size_t)nids * 4))) return r;
+    if ((r = upload(c, c->bsp_ref_tree, tree, (size_t)nnodes * 16))) return r;
+    if ((r = upload(c, c->bsp_ref_planes, planes, (size_t)nnodes * 4))) return r;
+    memcpy(c->bsp_aabb8, aabb, sizeof c->bsp_aabb8);
+    c->bsp_nnodes = nnodes;
+    c->bsp_nids = nids;
     c->bsp_depth = max_depth;
     c->aabb[0] = aabb[0];
     c->aabb[1] = aabb[1];
@@ -602,6 +610,75 @@ int rt_build_bvh_device(rt_ctx* c, uint32_t max_prims, rt_bvh_build_times* times
     c->bvh_nnodes = o.nnodes;
     c->bvh_nids = o.nids;
     c->has_bvh = true;
+    return RT_OK;
+}
+
+int rt_build_bsp_device(rt_ctx* c, uint32_t max_depth, uint32_t max_leaf, rt_bsp_build_times* times)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_build_bsp_device: upload the mesh first");
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->has_bsp = false;
+    rtk::BspDeviceOut o;
+    std::string err;
+    const int r = rtk::build_bsp_device(c->pos.as<float4>(), c->idx.as<uint4>(), c->ntris, max_depth, max_leaf,
+                                        c->num_cus, c->stream, o, times, err);
+    DevBuf tree, planes, ids;   // own the outputs from here on
+    if (o.tree) tree.adopt(o.tree, (size_t)o.nnodes * 16);
+    if (o.planes) planes.adopt(o.planes, (size_t)o.nnodes * 4);
+    if (o.ids) ids.adopt(o.ids, std::max<size_t>(16, (size_t)o.nids * 4));
+    if (r) return fail(c, r, err);
+    const size_t slots = (size_t)o.nnodes + 1;
+    const size_t rec_off = (slots * 64 + 255) & ~(size_t)255;
+    const size_t total = rec_off + (size_t)o.nids * 48;
+    if (total >= ((size_t)1 << 32))
+        return fail(c, RT_E_UNSUPPORTED, "rt_build_bsp_device: BSP treelets + records must stay below 4 GiB");
+    HIPCHK(c, c->bsp_nodes.alloc(total));
+    if (rtk::launch_bsp_repack(tree.as<uint32_t>(), planes.as<float>(), o.nnodes, (uint32_t)rec_off, c->bsp_nodes.p,
+                               c->pos.as<float4>(), c->idx.as<uint4>(), ids.as<uint32_t>(), o.nids, c->stream))
+        return fail(c, RT_E_DEVICE, "rt_build_bsp_device: repack launch failed");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->bsp_ref_tree.adopt(tree.p, tree.n);
+    tree.p = nullptr;
+    c->bsp_ref_planes.adopt(planes.p, planes.n);
+    planes.p = nullptr;
+    c->bsp_ids.adopt(ids.p, ids.n);
+    ids.p = nullptr;
+    c->bsp_rec_off = (uint32_t)rec_off;
+    c->bsp_depth = max_depth;
+    memcpy(c->bsp_aabb8, o.aabb, sizeof c->bsp_aabb8);
+    c->aabb[0] = o.aabb[0];
+    c->aabb[1] = o.aabb[1];
+    c->aabb[2] = o.aabb[2];
+    c->aabb[3] = o.aabb[4];
+    c->aabb[4] = o.aabb[5];
+    c->aabb[5] = o.aabb[6];
+    c->bsp_nnodes = o.nnodes;
+    c->bsp_nids = o.nids;
+    c->has_bsp = true;
+    return RT_OK;
+}
+
+int rt_download_bsp(rt_ctx* c, uint32_t* tree, float* planes, uint32_t cap_nodes, uint32_t* ids, uint32_t cap_ids,
+                    float aabb[8], uint32_t* nnodes, uint32_t* nids)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_download_bsp: no BSP on the context");
+    if (nnodes) *nnodes = c->bsp_nnodes;
+    if (nids) *nids = c->bsp_nids;
+    if (aabb) memcpy(aabb, c->bsp_aabb8, sizeof c->bsp_aabb8);
+    if (int r = set_dev(c)) return r;
+    if ((tree || planes) && cap_nodes < c->bsp_nnodes) return fail(c, RT_E_INVALID, "rt_download_bsp: arrays too small");
+    if (ids && cap_ids < c->bsp_nids) return fail(c, RT_E_INVALID, "rt_download_bsp: id array too small");
+    if (tree)
+        HIPCHK(c, hipMemcpyAsync(tree, c->bsp_ref_tree.p, (size_t)c->bsp_nnodes * 16, hipMemcpyDeviceToHost, c->stream));
+    if (planes)
+        HIPCHK(c, hipMemcpyAsync(planes, c->bsp_ref_planes.p, (size_t)c->bsp_nnodes * 4, hipMemcpyDeviceToHost,
+                                 c->stream));
+    if (ids && c->bsp_nids)
+        HIPCHK(c, hipMemcpyAsync(ids, c->bsp_ids.p, (size_t)c->bsp_nids * 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
     return RT_OK;
 }
 

@@ -1,0 +1,696 @@
+// rt_bsp_build.hip -- BSP construction on the GPU:
+// BspTree::new + bsp_array + primitive_ids (src/data_structures/bsp_tree.rs:
+// 45-189, subdivide_node :195-323) producing the same arrays as the host
+// builder (host_bsp.cpp, pinned to the oracle and the reference's JS builder).
+//
+// subdivide_node is breadth-first here: one pass per depth over every node of
+// that depth, with the node's objects as one contiguous segment of a per-level
+// slot array (in the reference's order).  Per level:
+//   k_bsp_count     the 9 candidate planes x (left, right) membership counts
+//                   of every splittable node (wave-level segmented popcounts,
+//                   block-level accumulation for the block's first node)
+//   k_bsp_decide    leaf test (:204), the strict-< min-cost candidate in
+//                   (axis, k) order (:220-249), leaf records
+//   k_bsp_extent    min lo / max hi along the chosen axis, only for nodes
+//                   with an empty side (:251-282)
+//   k_bsp_finalize  the moved plane, bsp_array node + plane
+//   k_bsp_flags     membership of every object in the two children (:293-300)
+//   scans           per-slot ranks, per-node child counts and child offsets
+//   k_bsp_children, k_bsp_scatter   next level's nodes and segments (left
+//                   child then right child, objects in order)
+// Finally the leaves are sorted into DFS order (key = branch << (D - depth))
+// and their first ids (:143-147) and primitive_ids (:79-101) follow from one
+// scan.  Node slots are fixed by (depth, branch) (idx = 2^depth + branch - 1),
+// so only the first ids depend on DFS order.
+// Numerics: the same f32 expressions as the host builder, -ffp-contract=off.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <string>
+#include <vector>
+
+#include "../../include/rt_detmath.h"
+#include "rt_internal.h"
+
+namespace rtbsp {
+
+struct LNode {                 // a node of the current level
+    uint32_t idx;              // bsp_array slot (0-based heap index)
+    uint32_t seg, cnt;         // its objects: slots[seg, seg + cnt)
+    uint32_t flags;            // 1: split, 2: needs the extent along its axis
+    float mn[3], mx[3];        // node box
+    uint32_t axis;
+    float plane;
+    uint32_t lnc, rnc;         // candidate counts (empty-side test)
+    uint32_t cntL, cntR;       // final child object counts
+    uint32_t child, cseg;      // next level: left child's node index and first slot
+};
+struct Leaf {
+    uint32_t idx, level, seg, cnt;
+};
+constexpr uint32_t F_SPLIT = 1u, F_EXT = 2u;
+
+__device__ __forceinline__ uint32_t ord_f(float f)   // monotone float -> u32 (non-NaN)
+{
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float unord_f(uint32_t u)
+{
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+__device__ __forceinline__ float area6(const float* mn, const float* mx)   // bbox.rs:117-125
+{
+    const float d0 = mx[0] - mn[0], d1 = mx[1] - mn[1], d2 = mx[2] - mn[2];
+    return 2.0f * (d0 * d1 + d1 * d2 + d2 * d0);
+}
+__device__ __forceinline__ bool isect(const float* smn, const float* smx, const float4 omn, const float4 omx)
+{   // bbox.rs:151-155, s.intersects(o)
+    return !(omn.x > smx[0] || omx.x < smn[0]) && !(omn.y > smx[1] || omx.y < smn[1]) &&
+           !(omn.z > smx[2] || omx.z < smn[2]);
+}
+__device__ __forceinline__ float comp4(const float4 v, uint32_t a) { return a == 0 ? v.x : (a == 1 ? v.y : v.z); }
+
+// ---- triangle boxes and the root box (Mesh::bboxes; BspTree::new :59-63)
+// The root box fold is evaluated as the reference's sequential fold: each
+// thread folds a contiguous range from Bbox::new(), and partial results are
+// combined left (earlier) to right in adjacent pairs, so ties keep the
+// earliest value exactly as include_bbox in index order does.
+__global__ void __launch_bounds__(256) k_tri_boxes(const float4* pos, const uint4* idx, uint32_t nt, uint32_t per,
+                                                   float4* boxes, float* partial)
+{
+    __shared__ float red[6][256];
+    const uint32_t t0 = (blockIdx.x * 256u + threadIdx.x) * per;
+    float bmn[3] = {1.0e37f, 1.0e37f, 1.0e37f}, bmx[3] = {-1.0e37f, -1.0e37f, -1.0e37f};
+    for (uint32_t t = t0; t < t0 + per && t < nt; t++) {
+        const uint4 ix = idx[t];
+        const float4 a = pos[ix.x], b = pos[ix.y], c = pos[ix.z];
+        const float mn[3] = {rt_minf(a.x, rt_minf(b.x, c.x)), rt_minf(a.y, rt_minf(b.y, c.y)),
+                             rt_minf(a.z, rt_minf(b.z, c.z))};
+        const float mx[3] = {rt_maxf(a.x, rt_maxf(b.x, c.x)), rt_maxf(a.y, rt_maxf(b.y, c.y)),
+                             rt_maxf(a.z, rt_maxf(b.z, c.z))};
+        boxes[2u * t] = make_float4(mn[0], mn[1], mn[2], 0.0f);
+        boxes[2u * t + 1u] = make_float4(mx[0], mx[1], mx[2], 0.0f);
+        for (int i = 0; i < 3; i++) {
+            bmn[i] = rt_minf(bmn[i], mn[i]);
+            bmx[i] = rt_maxf(bmx[i], mx[i]);
+        }
+    }
+    for (int i = 0; i < 3; i++) {
+        red[i][threadIdx.x] = bmn[i];
+        red[3 + i][threadIdx.x] = bmx[i];
+    }
+    __syncthreads();
+    for (uint32_t s = 1; s < 256u; s <<= 1) {   // adjacent pairs: [t] op [t+s], t % 2s == 0
+        if ((threadIdx.x & (2u * s - 1u)) == 0u)
+            for (int i = 0; i < 3; i++) {
+                red[i][threadIdx.x] = rt_minf(red[i][threadIdx.x], red[i][threadIdx.x + s]);
+                red[3 + i][threadIdx.x] = rt_maxf(red[3 + i][threadIdx.x], red[3 + i][threadIdx.x + s]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) partial[blockIdx.x * 6u + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// final fold of the per-block partials (in block order) into the root node
+__global__ void k_root(const float* partial, uint32_t nparts, uint32_t nt, LNode* nodes, uint32_t* slots,
+                       uint32_t* nos, float* aabb)
+{
+    if (threadIdx.x != 0) return;
+    float v[6] = {1.0e37f, 1.0e37f, 1.0e37f, -1.0e37f, -1.0e37f, -1.0e37f};
+    for (uint32_t p = 0; p < nparts; p++)
+        for (int i = 0; i < 3; i++) {
+            v[i] = rt_minf(v[i], partial[p * 6u + i]);
+            v[3 + i] = rt_maxf(v[3 + i], partial[p * 6u + 3 + i]);
+        }
+    LNode r;
+    r.idx = 0;
+    r.seg = 0;
+    r.cnt = nt;
+    r.flags = 0;
+    for (int i = 0; i < 3; i++) {
+        r.mn[i] = v[i];
+        r.mx[i] = v[3 + i];
+    }
+    r.axis = 0;
+    r.plane = 0.0f;
+    r.lnc = r.rnc = r.cntL = r.cntR = r.child = r.cseg = 0;
+    nodes[0] = r;
+    aabb[0] = v[0];
+    aabb[1] = v[1];
+    aabb[2] = v[2];
+    aabb[3] = 0.0f;
+    aabb[4] = v[3];
+    aabb[5] = v[4];
+    aabb[6] = v[5];
+    aabb[7] = 0.0f;
+}
+
+__global__ void __launch_bounds__(256) k_iota(uint32_t* slots, uint32_t* nos, uint32_t n)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+        slots[i] = i;
+        nos[i] = 0;
+    }
+}
+
+__device__ __forceinline__ bool splittable(const LNode& nd, uint32_t depth, uint32_t max_depth, uint32_t max_leaf)
+{
+    return !(nd.cnt <= max_leaf || depth == max_depth);   // :204
+}
+
+// ---- candidate counts: 18 per node, counts[node * 18 + c], c = axis*3 + (k-1) (left), 9 + ... (right)
+constexpr uint32_t kSlotsPerBlock = 4096;   // 4 waves x 16 rounds x 64
+__global__ void __launch_bounds__(256) k_bsp_count(const uint32_t* slots, const uint32_t* nos, uint32_t n,
+                                                   const LNode* nodes, const float4* boxes, uint32_t depth,
+                                                   uint32_t max_depth, uint32_t max_leaf, uint32_t* counts)
+{
+    __shared__ uint32_t acc[18];
+    const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+    const uint32_t base = blockIdx.x * kSlotsPerBlock;
+    if (threadIdx.x < 18) acc[threadIdx.x] = 0;
+    __syncthreads();
+    const uint32_t first = nos[base];   // base < n by the grid
+    for (uint32_t r = 0; r < 16u; r++) {
+        const uint32_t slot = base + wave * 1024u + r * 64u + lane;
+        const bool valid = slot < n;
+        const uint32_t node = valid ? nos[slot] : 0xFFFFFFFFu;
+        uint32_t bits = 0;
+        if (valid) {
+            const LNode& nd = nodes[node];
+            if (splittable(nd, depth, max_depth, max_leaf)) {
+                const uint32_t o = slots[slot];
+                const float4 omn = boxes[2u * o], omx = boxes[2u * o + 1u];
+                const bool ok0 = !(omn.x > nd.mx[0] || omx.x < nd.mn[0]);
+                const bool ok1 = !(omn.y > nd.mx[1] || omx.y < nd.mn[1]);
+                const bool ok2 = !(omn.z > nd.mx[2] || omx.z < nd.mn[2]);
+                for (uint32_t i = 0; i < 3; i++) {
+                    const bool others = (i == 0 ? ok1 && ok2 : (i == 1 ? ok0 && ok2 : ok0 && ok1));
+                    const float lo = comp4(omn, i), hi = comp4(omx, i);
+                    for (uint32_t k = 1; k < 4; k++) {
+                        const float c = (nd.mx[i] - nd.mn[i]) * (float)k / (float)4 + nd.mn[i];
+                        const bool inl = others && !(lo > c || hi < nd.mn[i]);
+                        const bool inr = others && !(lo > nd.mx[i] || hi < c);
+                        bits |= (inl ? 1u : 0u) << (i * 3u + k - 1u);
+                        bits |= (inr ? 1u : 0u) << (9u + i * 3u + k - 1u);
+                    }
+                }
+            }
+        }
+        const uint32_t prev = __shfl_up(node, 1, 64);
+        const bool head = valid && (lane == 0 || prev != node);
+        const uint64_t heads = __ballot(head);
+        const uint64_t vmask = __ballot(valid);
+        uint64_t seg = 0;
+        if (head) {
+            const uint64_t above = lane == 63 ? 0ull : (heads >> (lane + 1u)) << (lane + 1u);
+            const uint32_t end = above ? (uint32_t)__ffsll((unsigned long long)above) - 1u : 64u;
+            const uint64_t upto = end >= 64u ? ~0ull : ((1ull << end) - 1ull);
+            seg = upto & ~((1ull << lane) - 1ull) & vmask;
+        }
+        for (uint32_t c = 0; c < 18u; c++) {
+            const uint64_t b = __ballot((bits >> c) & 1u);
+            if (head && b) {
+                const uint32_t cnt = (uint32_t)__popcll(b & seg);
+                if (cnt) {
+                    if (node == first) atomicAdd(&acc[c], cnt);
+                    else atomicAdd(&counts[(size_t)node * 18u + c], cnt);
+                }
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 18 && acc[threadIdx.x]) atomicAdd(&counts[(size_t)first * 18u + threadIdx.x], acc[threadIdx.x]);
+}
+
+// ---- leaf test and the candidate choice (:204-249); leaves are final here
+__global__ void __launch_bounds__(256) k_bsp_decide(LNode* nodes, uint32_t nn, const uint32_t* counts, uint32_t depth,
+                                                    uint32_t max_depth, uint32_t max_leaf, uint32_t* tree,
+                                                    float* planes, uint32_t* ext, Leaf* leaves, uint32_t* leaf_keys,
+                                                    uint32_t* leaf_ctr)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nn; i += gridDim.x * 256u) {
+        LNode nd = nodes[i];
+        uint32_t* t = tree + 4u * (size_t)nd.idx;
+        t[1] = 0u;
+        t[2] = 2u * nd.idx + 1u;
+        t[3] = 2u * nd.idx + 2u;
+        planes[nd.idx] = 0.0f;
+        if (!splittable(nd, depth, max_depth, max_leaf)) {
+            t[0] = 3u + (nd.cnt << 2);
+            const uint32_t li = atomicAdd(leaf_ctr, 1u);
+            leaves[li] = Leaf{nd.idx, depth, nd.seg, nd.cnt};
+            const uint32_t branch = nd.idx + 1u - (1u << depth);
+            leaf_keys[li] = branch << (max_depth - depth);   // DFS order of the leaves
+            nd.flags = 0;
+            nodes[i] = nd;
+            continue;
+        }
+        const uint32_t* cn = counts + (size_t)i * 18u;
+        uint32_t axis_leaf = 0, lnc = 0, rnc = 0;
+        float plane = 0.0f, min_cost = 1E+27f;
+        for (uint32_t a = 0; a < 3; a++)
+            for (uint32_t k = 1; k < 4; k++) {
+                float lmn[3] = {nd.mn[0], nd.mn[1], nd.mn[2]}, lmx[3] = {nd.mx[0], nd.mx[1], nd.mx[2]};
+                float rmn[3] = {nd.mn[0], nd.mn[1], nd.mn[2]}, rmx[3] = {nd.mx[0], nd.mx[1], nd.mx[2]};
+                const float c = (nd.mx[a] - nd.mn[a]) * (float)k / (float)4 + nd.mn[a];
+                lmx[a] = c;
+                rmn[a] = c;
+                const uint32_t lc = cn[a * 3u + k - 1u], rc = cn[9u + a * 3u + k - 1u];
+                const float cost = (float)(int32_t)lc * area6(lmn, lmx) + (float)(int32_t)rc * area6(rmn, rmx);
+                if (cost < min_cost) {
+                    min_cost = cost;
+                    axis_leaf = a;
+                    plane = c;
+                    lnc = lc;
+                    rnc = rc;
+                }
+            }
+        nd.axis = axis_leaf;
+        nd.plane = plane;
+        nd.lnc = lnc;
+        nd.rnc = rnc;
+        nd.flags = F_SPLIT | ((lnc == 0u || rnc == 0u) ? F_EXT : 0u);
+        ext[2u * i] = ord_f(nd.mx[axis_leaf]);        // lnc == 0: min(max_corner, objects' lo)
+        ext[2u * i + 1u] = ord_f(nd.mn[axis_leaf]);   // rnc == 0: max(min_corner, objects' hi)
+        nodes[i] = nd;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_bsp_extent(const uint32_t* slots, const uint32_t* nos, uint32_t n,
+                                                    const LNode* nodes, const float4* boxes, uint32_t* ext)
+{
+    for (uint32_t s = blockIdx.x * 256u + threadIdx.x; s < n; s += gridDim.x * 256u) {
+        const uint32_t node = nos[s];
+        const LNode& nd = nodes[node];
+        if (!(nd.flags & F_EXT)) continue;
+        const uint32_t o = slots[s];
+        if (nd.lnc == 0u) atomicMin(&ext[2u * node], ord_f(comp4(boxes[2u * o], nd.axis)));
+        if (nd.rnc == 0u) atomicMax(&ext[2u * node + 1u], ord_f(comp4(boxes[2u * o + 1u], nd.axis)));
+    }
+}
+
+// the moved plane (:251-282) and the split node's bsp_array entry
+__global__ void __launch_bounds__(256) k_bsp_finalize(LNode* nodes, uint32_t nn, const uint32_t* ext, uint32_t* tree,
+                                                      float* planes)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nn; i += gridDim.x * 256u) {
+        LNode nd = nodes[i];
+        if (!(nd.flags & F_SPLIT)) continue;
+        const float max_corner = nd.mx[nd.axis], min_corner = nd.mn[nd.axis];
+        const float size = max_corner - min_corner;
+        const float diff = 1e-6f < (size / 8.0f) ? size / 8.0f : 1e-6f;
+        float center = nd.plane;
+        if (nd.lnc == 0u) center = unord_f(ext[2u * i]) - diff;
+        if (nd.rnc == 0u) center = unord_f(ext[2u * i + 1u]) + diff;
+        nd.plane = center;
+        tree[4u * (size_t)nd.idx] = nd.axis + (nd.cnt << 2);
+        planes[nd.idx] = center;
+        nodes[i] = nd;
+    }
+}
+
+// membership in the two children (:293-300): fl/fr[slot] in {0, 1}; fl[n] = fr[n] = 0
+__global__ void __launch_bounds__(256) k_bsp_flags(const uint32_t* slots, const uint32_t* nos, uint32_t n,
+                                                   const LNode* nodes, const float4* boxes, uint32_t* fl, uint32_t* fr)
+{
+    for (uint32_t s = blockIdx.x * 256u + threadIdx.x; s <= n; s += gridDim.x * 256u) {
+        uint32_t l = 0, r = 0;
+        if (s < n) {
+            const LNode& nd = nodes[nos[s]];
+            if (nd.flags & F_SPLIT) {
+                const uint32_t o = slots[s];
+                const float4 omn = boxes[2u * o], omx = boxes[2u * o + 1u];
+                float lmx[3] = {nd.mx[0], nd.mx[1], nd.mx[2]}, rmn[3] = {nd.mn[0], nd.mn[1], nd.mn[2]};
+                lmx[nd.axis] = nd.plane;
+                rmn[nd.axis] = nd.plane;
+                l = isect(nd.mn, lmx, omn, omx) ? 1u : 0u;
+                r = isect(rmn, nd.mx, omn, omx) ? 1u : 0u;
+            }
+        }
+        fl[s] = l;
+        fr[s] = r;
+    }
+}
+
+// child object counts from the scanned flags; a[i] = 2 children, b[i] = their objects
+__global__ void __launch_bounds__(256) k_bsp_child_counts(LNode* nodes, uint32_t nn, const uint32_t* el,
+                                                          const uint32_t* er, uint32_t* a, uint32_t* b)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i <= nn; i += gridDim.x * 256u) {
+        if (i == nn) {
+            a[i] = 0;
+            b[i] = 0;
+            continue;
+        }
+        LNode nd = nodes[i];
+        if (!(nd.flags & F_SPLIT)) {
+            a[i] = 0;
+            b[i] = 0;
+            continue;
+        }
+        nd.cntL = el[nd.seg + nd.cnt] - el[nd.seg];
+        nd.cntR = er[nd.seg + nd.cnt] - er[nd.seg];
+        a[i] = 2;
+        b[i] = nd.cntL + nd.cntR;
+        nodes[i] = nd;
+    }
+}
+
+// next level's nodes: left child then right child, boxes split at the plane
+__global__ void __launch_bounds__(256) k_bsp_children(LNode* nodes, uint32_t nn, const uint32_t* ea, const uint32_t* eb,
+                                                      LNode* next)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nn; i += gridDim.x * 256u) {
+        LNode nd = nodes[i];
+        if (!(nd.flags & F_SPLIT)) continue;
+        nd.child = ea[i];
+        nd.cseg = eb[i];
+        nodes[i] = nd;
+        LNode l, r;
+        for (int k = 0; k < 3; k++) {
+            l.mn[k] = r.mn[k] = nd.mn[k];
+            l.mx[k] = r.mx[k] = nd.mx[k];
+        }
+        l.mx[nd.axis] = nd.plane;
+        r.mn[nd.axis] = nd.plane;
+        l.idx = 2u * nd.idx + 1u;
+        r.idx = 2u * nd.idx + 2u;
+        l.seg = nd.cseg;
+        l.cnt = nd.cntL;
+        r.seg = nd.cseg + nd.cntL;
+        r.cnt = nd.cntR;
+        l.flags = r.flags = 0;
+        l.axis = r.axis = 0;
+        l.plane = r.plane = 0.0f;
+        l.lnc = l.rnc = l.cntL = l.cntR = l.child = l.cseg = 0;
+        r.lnc = r.rnc = r.cntL = r.cntR = r.child = r.cseg = 0;
+        next[nd.child] = l;
+        next[nd.child + 1u] = r;
+    }
+}
+
+__global__ void __launch_bounds__(256) k_bsp_scatter(const uint32_t* slots, const uint32_t* nos, uint32_t n,
+                                                     const LNode* nodes, const uint32_t* el, const uint32_t* er,
+                                                     uint32_t* nslots, uint32_t* nnos)
+{
+    for (uint32_t s = blockIdx.x * 256u + threadIdx.x; s < n; s += gridDim.x * 256u) {
+        const LNode& nd = nodes[nos[s]];
+        if (!(nd.flags & F_SPLIT)) continue;
+        const uint32_t o = slots[s];
+        if (el[s + 1u] != el[s]) {
+            const uint32_t p = nd.cseg + (el[s] - el[nd.seg]);
+            nslots[p] = o;
+            nnos[p] = nd.child;
+        }
+        if (er[s + 1u] != er[s]) {
+            const uint32_t p = nd.cseg + nd.cntL + (er[s] - er[nd.seg]);
+            nslots[p] = o;
+            nnos[p] = nd.child + 1u;
+        }
+    }
+}
+
+// ---- flatten: leaves in DFS order -> first ids and primitive_ids
+__global__ void __launch_bounds__(256) k_leaf_counts(const Leaf* leaves, const uint32_t* order, uint32_t nl,
+                                                     uint32_t* cnt)
+{
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < nl; j += gridDim.x * 256u) cnt[j] = leaves[order[j]].cnt;
+}
+
+__global__ void __launch_bounds__(256) k_leaf_finish(const Leaf* leaves, const uint32_t* order, uint32_t nl,
+                                                     const uint32_t* first, uint32_t* const* level_slots,
+                                                     uint32_t* tree, uint32_t* ids)
+{
+    for (uint32_t j = blockIdx.x * 256u + threadIdx.x; j < nl; j += gridDim.x * 256u) {
+        const Leaf lf = leaves[order[j]];
+        const uint32_t f = first[j];
+        tree[4u * (size_t)lf.idx + 1u] = f;
+        const uint32_t* src = level_slots[lf.level] + lf.seg;
+        for (uint32_t t = 0; t < lf.cnt; t++) ids[f + t] = src[t];
+    }
+}
+
+}  // namespace rtbsp
+
+namespace rtk {
+
+// rt_upload_bsp's repack on device: the 64-B treelet of every 1-based node M
+// (nodes M, 2M, 2M+1, 4M..4M+3 as 8-B entries) and the 48-B triangle records.
+__global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes,
+                                                    uint32_t rec_off, uint2* tl)
+{
+    const size_t slots = (size_t)nnodes + 1;
+    for (size_t m = (size_t)blockIdx.x * 256u + threadIdx.x; m < slots; m += (size_t)gridDim.x * 256u) {
+        auto node8 = [&](size_t q) -> uint2 {
+            if (q == 0 || q > nnodes) return make_uint2(0u, 0u);
+            const uint32_t* n = tree + 4 * (q - 1);
+            if ((n[0] & 3u) == 3u) return make_uint2(3u | ((48u * (n[0] >> 2)) << 2), rec_off + 48u * n[1]);
+            return make_uint2(n[0] & 3u, __float_as_uint(planes[q - 1]));
+        };
+        uint2* o = tl + 8 * m;
+        if (m == 0) {
+            for (int k = 0; k < 8; k++) o[k] = make_uint2(0u, 0u);
+            continue;
+        }
+        o[0] = node8(m);
+        o[1] = node8(2 * m);
+        o[2] = node8(2 * m + 1);
+        o[3] = make_uint2(0u, 0u);
+        o[4] = node8(4 * m);
+        o[5] = node8(4 * m + 1);
+        o[6] = node8(4 * m + 2);
+        o[7] = node8(4 * m + 3);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_tri_records2(const float4* pos, const uint4* idx, const uint32_t* ids,
+                                                      uint32_t nids, float4* recs)
+{
+    for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < nids; k += gridDim.x * 256u) {
+        const uint4 ix = idx[ids[k]];
+        const float4 a = pos[ix.x], b = pos[ix.y], c = pos[ix.z];
+        const float e0[3] = {b.x - a.x, b.y - a.y, b.z - a.z};
+        const float e1[3] = {c.x - a.x, c.y - a.y, c.z - a.z};
+        const float n[3] = {e0[1] * e1[2] - e0[2] * e1[1], e0[2] * e1[0] - e0[0] * e1[2], e0[0] * e1[1] - e0[1] * e1[0]};
+        recs[3u * k] = make_float4(a.x, a.y, a.z, e0[0]);
+        recs[3u * k + 1u] = make_float4(e0[1], e0[2], e1[0], e1[1]);
+        recs[3u * k + 2u] = make_float4(e1[2], n[0], n[1], n[2]);
+    }
+}
+
+int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
+                      const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, hipStream_t s)
+{
+    const uint32_t g1 = std::min<uint32_t>(16384, (nnodes + 256) / 256 + 1);
+    hipLaunchKernelGGL(k_bsp_repack, dim3(g1), dim3(256), 0, s, tree, planes, nnodes, rec_off,
+                       reinterpret_cast<uint2*>(blob));
+    if (nids) {
+        const uint32_t g2 = std::min<uint32_t>(16384, (nids + 255) / 256 + 1);
+        hipLaunchKernelGGL(k_tri_records2, dim3(g2), dim3(256), 0, s, pos, idx, ids, nids,
+                           reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(blob) + rec_off));
+    }
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+
+namespace {
+struct DBufs {   // device allocations freed at scope exit
+    std::vector<void*> p;
+    hipError_t e = hipSuccess;
+    ~DBufs()
+    {
+        for (void* q : p) (void)hipFree(q);
+    }
+    template <class T>
+    T* alloc(size_t count)
+    {
+        void* q = nullptr;
+        if (e == hipSuccess) e = hipMalloc(&q, std::max<size_t>(16, count * sizeof(T)));
+        if (e == hipSuccess) p.push_back(q);
+        return reinterpret_cast<T*>(q);
+    }
+};
+inline uint32_t blocks_for(size_t n, uint32_t cap) { return (uint32_t)std::max<size_t>(1, std::min<size_t>(cap, (n + 255) / 256)); }
+}  // namespace
+
+int build_bsp_device(const float4* pos, const uint4* idx, uint32_t nt, uint32_t max_depth, uint32_t max_leaf,
+                     int num_cus, hipStream_t s, BspDeviceOut& out, rt_bsp_build_times* times, std::string& err)
+{
+    using namespace rtbsp;
+    if (nt == 0) {
+        err = "rt_build_bsp_device: empty mesh";
+        return RT_E_INVALID;
+    }
+    if (max_depth == 0 || max_depth > 24 || max_leaf == 0) {
+        err = "rt_build_bsp_device: max_depth must be in [1,24] (the traversal layout's limit), max_leaf > 0";
+        return RT_E_INVALID;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t cap = (uint32_t)std::max(1, num_cus) * 16u;
+    const size_t nnodes = ((size_t)1 << (max_depth + 1)) - 1;
+    DBufs D;
+    float4* boxes = D.alloc<float4>((size_t)nt * 2);
+    const uint32_t per = (nt + 65535u) / 65536u;   // triangles per thread: <= 256 blocks of contiguous ranges
+    const uint32_t rblocks = (nt + 256u * per - 1) / (256u * per);
+    float* partial = D.alloc<float>((size_t)rblocks * 6);
+    uint32_t* leaf_ctr = D.alloc<uint32_t>(4);
+    Leaf* leaves = D.alloc<Leaf>(nnodes);
+    uint32_t* lkeys = D.alloc<uint32_t>(nnodes);
+    uint32_t* d_aabb_u = D.alloc<uint32_t>(8);
+    if (D.e != hipSuccess) {
+        err = std::string("rt_build_bsp_device: allocation: ") + hipGetErrorString(D.e);
+        return RT_E_OOM;
+    }
+    if (hipMalloc(&out.tree, nnodes * 16) != hipSuccess || hipMalloc(&out.planes, nnodes * 4) != hipSuccess) {
+        err = "rt_build_bsp_device: output allocation failed";
+        return RT_E_OOM;
+    }
+    out.nnodes = (uint32_t)nnodes;
+    (void)hipMemsetAsync(out.tree, 0, nnodes * 16, s);   // unused slots (0,0,0,0) / plane 0
+    (void)hipMemsetAsync(out.planes, 0, nnodes * 4, s);
+    (void)hipMemsetAsync(leaf_ctr, 0, 16, s);
+    // level 0
+    std::vector<uint32_t*> level_slots;
+    uint32_t nn = 1, ns = nt;
+    LNode* nodes = D.alloc<LNode>(1);
+    uint32_t* slots = D.alloc<uint32_t>(ns);
+    uint32_t* nos = D.alloc<uint32_t>(ns);
+    hipLaunchKernelGGL(k_tri_boxes, dim3(rblocks), dim3(256), 0, s, pos, idx, nt, per, boxes, partial);
+    hipLaunchKernelGGL(k_iota, dim3(blocks_for(ns, cap)), dim3(256), 0, s, slots, nos, ns);
+    hipLaunchKernelGGL(k_root, dim3(1), dim3(64), 0, s, partial, rblocks, nt, nodes, slots, nos,
+                       reinterpret_cast<float*>(d_aabb_u));
+    uint32_t levels = 0;
+    for (uint32_t depth = 0; depth <= max_depth && nn > 0; depth++) {
+        levels++;
+        level_slots.push_back(slots);
+        uint32_t* counts = D.alloc<uint32_t>((size_t)nn * 18);
+        uint32_t* ext = D.alloc<uint32_t>((size_t)nn * 2);
+        uint32_t* el = D.alloc<uint32_t>((size_t)ns + 2);   // scans of ns+1 flags: ns+2 words
+        uint32_t* er = D.alloc<uint32_t>((size_t)ns + 2);
+        uint32_t* na = D.alloc<uint32_t>((size_t)nn + 2);
+        uint32_t* nb = D.alloc<uint32_t>((size_t)nn + 2);
+        uint32_t* sc = D.alloc<uint32_t>(scan_scratch_words(std::max(ns, nn) + 1));
+        if (D.e != hipSuccess) {
+            err = std::string("rt_build_bsp_device: level allocation: ") + hipGetErrorString(D.e);
+            return RT_E_OOM;
+        }
+        (void)hipMemsetAsync(counts, 0, (size_t)nn * 18 * 4, s);
+        if (ns > 0) {
+            const uint32_t cblocks = (ns + kSlotsPerBlock - 1) / kSlotsPerBlock;
+            hipLaunchKernelGGL(k_bsp_count, dim3(cblocks), dim3(256), 0, s, slots, nos, ns, nodes, boxes, depth,
+                               max_depth, max_leaf, counts);
+        }
+        hipLaunchKernelGGL(k_bsp_decide, dim3(blocks_for(nn, cap)), dim3(256), 0, s, nodes, nn, counts, depth,
+                           max_depth, max_leaf, out.tree, out.planes, ext, leaves, lkeys, leaf_ctr);
+        hipLaunchKernelGGL(k_bsp_extent, dim3(blocks_for(ns, cap)), dim3(256), 0, s, slots, nos, ns, nodes, boxes,
+                           ext);
+        hipLaunchKernelGGL(k_bsp_finalize, dim3(blocks_for(nn, cap)), dim3(256), 0, s, nodes, nn, ext, out.tree,
+                           out.planes);
+        hipLaunchKernelGGL(k_bsp_flags, dim3(blocks_for((size_t)ns + 1, cap)), dim3(256), 0, s, slots, nos, ns, nodes,
+                           boxes, el, er);
+        int r = scan_exclusive_u32(el, el, ns + 1, sc, s);
+        if (!r) r = scan_exclusive_u32(er, er, ns + 1, sc, s);
+        hipLaunchKernelGGL(k_bsp_child_counts, dim3(blocks_for((size_t)nn + 1, cap)), dim3(256), 0, s, nodes, nn, el,
+                           er, na, nb);
+        if (!r) r = scan_exclusive_u32(na, na, nn + 1, sc, s);
+        if (!r) r = scan_exclusive_u32(nb, nb, nn + 1, sc, s);
+        uint32_t tot[2] = {0, 0};
+        hipError_t e = hipGetLastError();
+        if (e == hipSuccess && !r) e = hipMemcpyAsync(&tot[0], na + nn + 1, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(&tot[1], nb + nn + 1, 4, hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess || r) {
+            err = std::string("rt_build_bsp_device: level ") + std::to_string(depth) + ": " + hipGetErrorString(e);
+            return RT_E_DEVICE;
+        }
+        const uint32_t nn2 = tot[0], ns2 = tot[1];
+        if (nn2 == 0) break;
+        LNode* next = D.alloc<LNode>(nn2);
+        uint32_t* nslots = D.alloc<uint32_t>(ns2);
+        uint32_t* nnos = D.alloc<uint32_t>(ns2);
+        if (D.e != hipSuccess) {
+            err = std::string("rt_build_bsp_device: level allocation: ") + hipGetErrorString(D.e);
+            return RT_E_OOM;
+        }
+        hipLaunchKernelGGL(k_bsp_children, dim3(blocks_for(nn, cap)), dim3(256), 0, s, nodes, nn, na, nb, next);
+        hipLaunchKernelGGL(k_bsp_scatter, dim3(blocks_for(ns, cap)), dim3(256), 0, s, slots, nos, ns, nodes, el, er,
+                           nslots, nnos);
+        nodes = next;
+        slots = nslots;
+        nos = nnos;
+        nn = nn2;
+        ns = ns2;
+    }
+    // ---- flatten: leaves in DFS order
+    uint32_t nl = 0;
+    if (hipMemcpyAsync(&nl, leaf_ctr, 4, hipMemcpyDeviceToHost, s) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        err = "rt_build_bsp_device: leaf count readback failed";
+        return RT_E_DEVICE;
+    }
+    const auto t1 = std::chrono::steady_clock::now();
+    uint32_t* ord = D.alloc<uint32_t>(nl);
+    uint32_t* k1 = D.alloc<uint32_t>(nl);
+    uint32_t* v1 = D.alloc<uint32_t>(nl);
+    uint32_t* hist = D.alloc<uint32_t>(radix_hist_words(nl));
+    uint32_t* lc = D.alloc<uint32_t>((size_t)nl + 1);
+    uint32_t* sc = D.alloc<uint32_t>(scan_scratch_words(nl + 1));
+    uint32_t** d_levels = D.alloc<uint32_t*>(level_slots.size());
+    if (D.e != hipSuccess) {
+        err = "rt_build_bsp_device: flatten allocation failed";
+        return RT_E_OOM;
+    }
+    (void)hipMemcpyAsync(d_levels, level_slots.data(), level_slots.size() * sizeof(uint32_t*), hipMemcpyHostToDevice, s);
+    if (nl) {
+        hipLaunchKernelGGL(k_iota, dim3(blocks_for(nl, cap)), dim3(256), 0, s, ord, v1, nl);
+        int second = 0;
+        const uint32_t passes = (max_depth + 7u) / 8u;   // keys < 2^max_depth
+        if (radix_sort_pairs(lkeys, ord, k1, v1, nl, passes, hist, s, second)) {
+            err = "rt_build_bsp_device: leaf sort failed";
+            return RT_E_DEVICE;
+        }
+        const uint32_t* order = second ? v1 : ord;
+        hipLaunchKernelGGL(k_leaf_counts, dim3(blocks_for(nl, cap)), dim3(256), 0, s, leaves, order, nl, lc);
+        (void)hipMemsetAsync(lc + nl, 0, 4, s);
+        if (scan_exclusive_u32(lc, lc, nl, sc, s)) {
+            err = "rt_build_bsp_device: leaf scan failed";
+            return RT_E_DEVICE;
+        }
+        uint32_t nids = 0;
+        if (hipMemcpyAsync(&nids, lc + nl, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            err = "rt_build_bsp_device: id count readback failed";
+            return RT_E_DEVICE;
+        }
+        if (hipMalloc(&out.ids, std::max<size_t>(16, (size_t)nids * 4)) != hipSuccess) {
+            err = "rt_build_bsp_device: id allocation failed";
+            return RT_E_OOM;
+        }
+        out.nids = nids;
+        hipLaunchKernelGGL(k_leaf_finish, dim3(blocks_for(nl, cap)), dim3(256), 0, s, leaves, order, nl, lc,
+                           d_levels, out.tree, out.ids);
+    } else if (hipMalloc(&out.ids, 16) != hipSuccess) {
+        return RT_E_OOM;
+    }
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpyAsync(out.aabb, d_aabb_u, 32, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        err = std::string("rt_build_bsp_device: flatten: ") + hipGetErrorString(e);
+        return RT_E_DEVICE;
+    }
+    if (times) {
+        const auto t2 = std::chrono::steady_clock::now();
+        times->subdivision_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        times->flattening_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        times->total_ms = std::chrono::duration<double, std::milli>(t2 - t0).count();
+        times->levels = levels;
+        times->leaves = nl;
+        times->nids = out.nids;
+    }
+    return RT_OK;
+}
+
+}  // namespace rtk

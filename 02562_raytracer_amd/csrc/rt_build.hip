@@ -440,9 +440,94 @@ __global__ void __launch_bounds__(256) k_set_dfs(const uint32_t* dfs, uint32_t n
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) pool[i].dfs = dfs[i];
 }
 
+// ------------------------------------------------------------ device-wide exclusive scan
+// out[0..n] = exclusive prefix sums of in[0..n), out[n] = total (in == out allowed).
+// Reduce-then-scan: 4096-element blocks (256 threads x 16), one-block scan of
+// the block sums, then each block scans its elements with its offset.
+constexpr uint32_t kScanBlock = 4096;
+__global__ void __launch_bounds__(256) k_scan_reduce(const uint32_t* in, uint32_t n, uint32_t* bsum)
+{
+    __shared__ uint32_t red[256];
+    const uint32_t base = blockIdx.x * kScanBlock;
+    uint32_t s = 0;
+    for (uint32_t i = threadIdx.x; i < kScanBlock; i += 256u)
+        if (base + i < n) s += in[base + i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t st = 128; st > 0; st >>= 1) {
+        if (threadIdx.x < st) red[threadIdx.x] += red[threadIdx.x + st];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) bsum[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) k_scan_down(const uint32_t* in, uint32_t n, const uint32_t* bsum,
+                                                   uint32_t* out)
+{
+    __shared__ uint32_t part[256];
+    const uint32_t base = blockIdx.x * kScanBlock + threadIdx.x * 16u;
+    uint32_t v[16], s = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        v[i] = base + i < n ? in[base + i] : 0u;
+        s += v[i];
+    }
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (uint32_t off = 1; off < 256u; off <<= 1) {
+        const uint32_t a = threadIdx.x >= off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += a;
+        __syncthreads();
+    }
+    uint32_t run = bsum[blockIdx.x] + part[threadIdx.x] - s;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+        if (base + i < n) out[base + i] = run;
+        run += v[i];
+    }
+    if (blockIdx.x == gridDim.x - 1u && threadIdx.x == 255u) out[n] = run;
+}
+
 }  // namespace rtb
 
 namespace rtk {
+
+int scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* scratch, hipStream_t s)
+{
+    using namespace rtb;
+    const uint32_t nb = n ? (n + kScanBlock - 1) / kScanBlock : 1;
+    if (n == 0) {
+        (void)hipMemsetAsync(out, 0, 4, s);
+        return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+    }
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(256), 0, s, in, n, scratch);
+    hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), 0, s, scratch, nb);
+    hipLaunchKernelGGL(k_scan_down, dim3(nb), dim3(256), 0, s, in, n, scratch, out);
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+size_t scan_scratch_words(uint32_t n) { return (size_t)(n + rtb::kScanBlock - 1) / rtb::kScanBlock + 16; }
+
+// Stable LSD radix sort of (key, value) pairs over the low 8*passes key bits;
+// ping-pongs between (k0,v0) and (k1,v1); returns which pair holds the result.
+int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, uint32_t passes,
+                     uint32_t* hist, hipStream_t s, int& result_in_second)
+{
+    using namespace rtb;
+    const uint32_t ntiles = (n + kTile - 1) / kTile;
+    result_in_second = 0;
+    for (uint32_t pass = 0; pass < passes && n; pass++) {
+        const uint32_t sh = pass * 8u;
+        hipLaunchKernelGGL(k_rs_hist, dim3(ntiles), dim3(256), 0, s, k0, n, sh, ntiles, hist);
+        hipLaunchKernelGGL(k_rs_scan, dim3(1), dim3(1024), 0, s, hist, 256u * ntiles);
+        hipLaunchKernelGGL(k_rs_scatter, dim3(ntiles), dim3(256), 0, s, k0, v0, n, sh, ntiles, hist, k1, v1);
+        std::swap(k0, k1);
+        std::swap(v0, v1);
+        result_in_second ^= 1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+size_t radix_hist_words(uint32_t n) { return (size_t)256 * ((n + rtb::kTile - 1) / rtb::kTile) + 16; }
 
 // Traversal layout (rt_api.cpp rt_upload_bvh): node record {min.xyz, w0}{max.xyz, w1}
 // with byte offsets, and 48-B triangle records {v0, e0, e1, n} in tri_ids order.

@@ -92,6 +92,27 @@ int build_bvh_device(const float4* pos, const uint4* idx, uint32_t ntris, uint32
 int launch_bvh_repack(const rt_gpu_node* nodes, uint32_t nnodes, uint32_t rec_off, void* blob, const float4* pos,
                       const uint4* idx, const uint32_t* ids, uint32_t nids, hipStream_t stream);
 
+// GPU BSP build (rt_bsp_build.hip): reference-layout arrays (bsp_array, planes,
+// primitive_ids, BboxGpu), device allocations owned by the caller afterwards.
+struct BspDeviceOut {
+    uint32_t* tree = nullptr;    // nnodes x vec4u
+    float* planes = nullptr;     // nnodes
+    uint32_t* ids = nullptr;     // nids
+    float aabb[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    uint32_t nnodes = 0, nids = 0;
+};
+int build_bsp_device(const float4* pos, const uint4* idx, uint32_t ntris, uint32_t max_depth, uint32_t max_leaf,
+                     int num_cus, hipStream_t stream, BspDeviceOut& out, rt_bsp_build_times* times, std::string& err);
+// traversal layout of a BSP from its reference-layout arrays (rt_upload_bsp's repack, on device)
+int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
+                      const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, hipStream_t stream);
+// device primitives shared by the builders (rt_build.hip)
+int scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* scratch, hipStream_t s);
+size_t scan_scratch_words(uint32_t n);
+int radix_sort_pairs(uint32_t* k0, uint32_t* v0, uint32_t* k1, uint32_t* v1, uint32_t n, uint32_t passes,
+                     uint32_t* hist, hipStream_t s, int& result_in_second);
+size_t radix_hist_words(uint32_t n);
+
 int launch_selftest_math(const float* in, float* out, uint32_t n, hipStream_t stream);
 
 // get_camera_ray's basis from the uniforms (host, same f32 operations as the shader)

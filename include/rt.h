@@ -256,6 +256,29 @@ typedef struct rt_bvh_build_times {
  * would.  times may be NULL.  Synchronizes the context stream. */
 int rt_build_bvh_device(rt_ctx* ctx, uint32_t max_prims, rt_bvh_build_times* times);
 
+/* Per-phase times of a device BSP build (src/bin/bvh_project.rs
+ * BspConstructionTime: subdivision, flattening). */
+typedef struct rt_bsp_build_times {
+    double subdivision_ms;   /* the level-by-level subdivide_node of every depth       */
+    double flattening_ms;    /* leaf first-ids in DFS order + primitive_ids            */
+    double total_ms;         /* wall clock of the whole call                           */
+    uint32_t levels, leaves, nids;
+} rt_bsp_build_times;
+
+/* BspTree::new(mesh.bboxes(), max_depth, max_leaf) + bsp_array() +
+ * primitive_ids() (src/data_structures/bsp_tree.rs:45-189, 195-323) on the
+ * device from the context's uploaded mesh: the same arrays as rt_bsp_build,
+ * installed as the context's BSP as rt_upload_bsp would.  Subdivision runs
+ * one depth level at a time over all nodes of that level.  times may be NULL.
+ * Synchronizes the context stream. */
+int rt_build_bsp_device(rt_ctx* ctx, uint32_t max_depth, uint32_t max_leaf, rt_bsp_build_times* times);
+
+/* Copy the context's BSP in the reference layout (bsp_array vec4u, planes,
+ * primitive_ids, BboxGpu aabb[8]) to host arrays; sizes stored in nnodes/nids
+ * (pass NULL arrays to query them). */
+int rt_download_bsp(rt_ctx* ctx, uint32_t* tree, float* planes, uint32_t cap_nodes, uint32_t* ids,
+                    uint32_t cap_ids, float aabb[8], uint32_t* nnodes, uint32_t* nids);
+
 /* Copy the context's BVH in the reference layout (GpuNode array, bvh_triangles)
  * to host arrays of capacity cap_nodes / cap_ids; the sizes are stored in
  * nnodes / nids (pass NULL arrays to query them). */

@@ -20,6 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 PUBLISHED_MS = {("teapot", 4): 0.993, ("bunny", 4): 4.305, ("dragon", 4): 49.28}   # benchmark.md:9-32
+PUBLISHED_BSP_MS = {"teapot": 31.47, "bunny": 144.38, "dragon": 827.93}   # benchmark.md:132-171 (depth 20, leaf 4)
 
 
 def main():
@@ -55,6 +56,29 @@ def main():
                 "treelets": int(acc["treelets"] / a.runs), "nodes": int(acc["nodes"] / a.runs),
                 "host_cpp_ms": round(host_ms, 3), "host_threads": os.cpu_count(),
                 "reference_published_cpu_ms": PUBLISHED_MS.get((name, mp))}
+        lines.append(line)
+        print(json.dumps(line), flush=True)
+    # BSP, depth 20 / leaf 4 (run_single_bsp, bvh_project.rs:90-106), plus the 10M soup of config 5
+    meshes["soup10M"] = rt.Mesh.synth_soup(10_000_000)
+    for name in ("teapot", "bunny", "dragon", "soup10M"):
+        mesh = meshes[name]
+        ctx.upload_mesh(mesh)
+        ctx.build_bsp_device(20, 4)   # warm-up
+        runs = a.runs if name != "soup10M" else 3
+        acc = {}
+        for _ in range(runs):
+            t = ctx.build_bsp_device(20, 4)
+            for k, v in t.items():
+                acc[k] = acc.get(k, 0.0) + v
+        gpu = {k: round(acc[k] / runs, 3) for k in ("subdivision_ms", "flattening_ms", "total_ms")}
+        t0 = time.perf_counter()
+        hruns = 1 if name == "soup10M" else max(1, runs // 4)
+        for _ in range(hruns):
+            mesh.bsp_tree(20, 4)
+        host_ms = (time.perf_counter() - t0) / hruns * 1e3
+        line = {"bsp_mesh": name, "ntris": mesh.ntris, "max_depth": 20, "max_leaf": 4, "runs": runs, "gpu_ms": gpu,
+                "leaves": int(acc["leaves"] / runs), "nids": int(acc["nids"] / runs),
+                "host_cpp_ms": round(host_ms, 2), "reference_published_cpu_ms": PUBLISHED_BSP_MS.get(name)}
         lines.append(line)
         print(json.dumps(line), flush=True)
     ctx.close()
