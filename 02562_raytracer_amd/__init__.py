@@ -10,10 +10,11 @@ The package directory name starts with a digit; import it with
 """
 from . import _ffi
 from ._ffi import MODES, TRAVERSALS, RtError, lib
-from .core import BspTree, Bvh, Context, DeviceBuffer, Mesh, local_tiles, make_uniform
+from .core import BspTree, Bvh, Context, DeviceBuffer, Mesh, load_texture_rgba8, local_tiles, make_uniform
 from .render_state import ASSETS, RenderState
 from .scenes import Camera, SceneDescriptor, find_scene, get_scenes
 
 __all__ = ["BspTree", "Bvh", "Camera", "Context", "DeviceBuffer", "Mesh", "RenderState", "RtError",
            "SceneDescriptor", "ASSETS", "MODES", "TRAVERSALS", "find_scene", "get_scenes", "lib", "local_tiles",
+           "load_texture_rgba8",
            "make_uniform", "_ffi"]

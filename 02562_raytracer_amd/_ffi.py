@@ -142,6 +142,7 @@ SIGNATURES = {
     "rt_upload_bvh": (C.c_int, [vp, C.POINTER(GpuNode), C.c_uint32, u32p, C.c_uint32]),
     "rt_set_uniforms": (C.c_int, [vp, C.POINTER(Uniform), f32p]),
     "rt_set_environment": (C.c_int, [vp, f32p]),
+    "rt_set_environment_map": (C.c_int, [vp, C.POINTER(C.c_uint8), C.c_uint32, C.c_uint32]),
     "rt_render": (C.c_int, [vp, C.c_int, C.c_int, C.POINTER(Tile), C.c_uint32, C.c_uint32, vp, vp,
                             C.POINTER(RayCounts)]),
     "rt_render_tiles": (C.c_int, [vp, C.c_int, C.c_int, C.POINTER(Tileset), C.c_uint32, C.c_uint32, vp, vp,

@@ -344,6 +344,18 @@ class Context:
         a = np.ascontiguousarray(rgb, dtype=np.float32)
         self._chk(F.lib().rt_set_environment(self._h, F.as_f32p(a)))
 
+    def set_environment_map(self, rgba8):
+        """hdri0 equirectangular background for W9E1: uint8[h, w, 4] (RGBA), or None."""
+        if rgba8 is None:
+            self._chk(F.lib().rt_set_environment_map(self._h, None, 0, 0))
+            return
+        a = np.ascontiguousarray(rgba8, dtype=np.uint8)
+        if a.ndim != 3 or a.shape[2] != 4:
+            raise ValueError("environment map must be uint8[h, w, 4]")
+        self._env_keep = a
+        self._chk(F.lib().rt_set_environment_map(self._h, a.ctypes.data_as(C.POINTER(C.c_uint8)), a.shape[1],
+                                                 a.shape[0]))
+
     def alloc(self, nbytes):
         return DeviceBuffer(self, nbytes)
 
@@ -395,6 +407,15 @@ class Context:
         bad = C.c_uint32()
         self._chk(F.lib().rt_selftest_math(self._h, n, lo, hi, C.byref(bad)))
         return bad.value
+
+
+def load_texture_rgba8(path):
+    """Texture::from_file (src/bindings/texture.rs:98, image.to_rgba8()): a
+    JPEG/PNG as uint8[h, w, 4].  Decoded with PIL (the reference's image 0.24
+    decoder is not available: texel values are parity-unpinned)."""
+    from PIL import Image
+    with Image.open(path) as im:
+        return np.asarray(im.convert("RGBA"), dtype=np.uint8).copy()
 
 
 def local_tiles(width, height, nranks):

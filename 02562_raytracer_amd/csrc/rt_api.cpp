@@ -92,6 +92,8 @@ struct rt_ctx {
     DevBuf jitter;
     bool has_jitter = false;
     float env[3] = {1.0f, 1.0f, 1.0f};
+    DevBuf env_tex;   // RGBA8 equirectangular hdri0 (rt_set_environment_map)
+    uint32_t env_w = 0, env_h = 0;
     DevBuf work, counters;
     rt_ray_counts last;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -753,6 +755,24 @@ static int launch_timed(rt_ctx* c, const rtk::DevScene& S, const rtk::DevLaunch&
     return RT_OK;
 }
 
+int rt_set_environment_map(rt_ctx* c, const uint8_t* rgba8, uint32_t width, uint32_t height)
+{
+    if (!c) return RT_E_INVALID;
+    if (!rgba8) {
+        c->env_tex.reset();
+        c->env_w = c->env_h = 0;
+        return RT_OK;
+    }
+    if (width == 0 || height == 0 || (uint64_t)width * height >= (1ull << 31))
+        return fail(c, RT_E_INVALID, "rt_set_environment_map: bad texture size");
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (int r = upload(c, c->env_tex, rgba8, (size_t)width * height * 4)) return r;
+    c->env_w = width;
+    c->env_h = height;
+    return RT_OK;
+}
+
 static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
 {
     if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
@@ -798,6 +818,9 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     rtk::camera_basis(c->u, L.cam);
     L.jitter = c->has_jitter ? c->jitter.as<float>() : nullptr;
     memcpy(L.env, c->env, sizeof L.env);
+    L.env_tex = c->env_w ? c->env_tex.as<uint32_t>() : nullptr;
+    L.env_w = c->env_w;
+    L.env_h = c->env_h;
     L.work_counter = c->work.as<uint32_t>();
     L.shade_threshold = (uint32_t)c->shade_threshold;
     L.min_half_lanes = c->min_half_lanes;

@@ -45,6 +45,8 @@ struct DevLaunch {
     float cam[14];                // camera basis e, v, b1, b2, d, aspect (get_camera_ray, w7e3.wgsl:211-228)
     const float* jitter;          // subdiv^2 float2 (device), may be null when subdiv == 1
     float env[3];
+    const uint32_t* env_tex;      // RGBA8 equirectangular hdri0, or null for the constant env
+    uint32_t env_w, env_h;
     // region mode (tileset == 0): 8x8 tiles over [x0,x0+w) x [y0,y0+h), row-major region output
     // tileset mode (tileset == 1): global 8x8 tiles t = l*nranks + rank, packed output
     uint32_t tileset;
@@ -121,6 +123,6 @@ void camera_basis(const rt_uniform& u, float cam[14]);
 // Host reference of the pinned math for the self test (same header, host compile).
 void host_math(const float* in, float* out, uint32_t n);
 
-constexpr int kMathOuts = 10;   // outputs per input in the math self test
+constexpr int kMathOuts = 12;   // outputs per input in the math self test
 
 }  // namespace rtk

@@ -835,7 +835,13 @@ k_path(DevScene S, DevLaunch L)
                     }
                 } else {
                     // miss: background (w7e3) / environment_map(dir) * factor (w9e1.wgsl:264-265)
-                    res = add(res, W9 ? mul(env, fac) : V(0, 0, 0));
+                    f3 e = env;
+                    if (W9 && L.env_tex) {
+                        float rgb[3];
+                        rt_det_env_sample(L.env_tex, L.env_w, L.env_h, rd.x, rd.y, rd.z, rgb);
+                        e = V(rgb[0], rgb[1], rgb[2]);
+                    }
+                    res = add(res, W9 ? mul(e, fac) : V(0, 0, 0));
                     sample_done = true;
                 }
             } else {
@@ -1229,6 +1235,8 @@ __host__ __device__ inline void math_eval(float x, float* o)
     const float dd = 0.13f + (x < 0.0f ? -x : x) * 0.2f, xx = x * 37.1f + 0.3f;   // the BSP walk's fast exact division
     o[8] = rt_div_by_recip(xx, dd, 1.0f / dd);
     o[9] = xx / dd;
+    o[10] = rt_det_atan2f(x, 1.3f - x * 0.9f);   // environment_map's atan2 (w9e1.wgsl:236)
+    o[11] = rt_det_atanf(x * 5.0f);
 }
 __global__ void k_selftest_math(const float* in, float* out, uint32_t n)
 {

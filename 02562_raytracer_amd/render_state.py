@@ -7,8 +7,9 @@ Differences from the windowed reference, all deliberate:
     uses the window's inner size, render_state.rs:563-566);
   * the accumulation "texture" is an HBM float4 array (linear RGBA32F), and
     the display transform pow(., 1.5) is left to the caller;
-  * the W9E1 equirectangular hdri0 is a constant environment colour
-    (rt_set_environment) -- texture sampling is out of scope (SURVEY.md 8(f));
+  * the W9E1 equirectangular hdri0 is the scene's background_hdri texture
+    when the file is in assets/textures (decoded with PIL, sampled as
+    include/rt_detmath.h pins it), else a constant environment colour;
   * a missing bunny.obj can be replaced by the deterministic stand-in
     (bunny_standin=True), since the reference checkout lacks it.
 """
@@ -25,16 +26,27 @@ ASSETS = os.path.join(REPO, "assets", "models")
 
 class RenderState:
     def __init__(self, scene, device=0, ctx=None, models_dir=ASSETS, bunny_standin=True, selection1=0,
-                 env=(1.0, 1.0, 1.0), resolution=None):
+                 env=(1.0, 1.0, 1.0), resolution=None, device_build=False):
         self.ctx = ctx if ctx is not None else Context(device)
         self.models_dir = models_dir
         self.bunny_standin = bunny_standin
         self.selection1 = selection1
         self.env = env
         self.resolution = resolution
+        self.device_build = device_build   # build the BSP / HLBVH on the GPU (same arrays)
         self.progressive = True
         self.iteration = 0
         self.setup_rendering(scene)
+
+    def _background(self, scene):
+        """render_state.rs:191-206: the scene's background_hdri, if present."""
+        if not getattr(scene, "background_hdri", None):
+            return None
+        path = os.path.join(REPO, "assets", "textures", os.path.basename(scene.background_hdri))
+        if not os.path.exists(path):
+            return None
+        from .core import load_texture_rgba8
+        return load_texture_rgba8(path)
 
     # render_state.rs:161-265
     def setup_rendering(self, scene):
@@ -51,12 +63,22 @@ class RenderState:
             self.mesh = self._load_model(scene.model)
             self.ctx.upload_mesh(self.mesh)
             if self.trav == "BSP":
-                self.bsp = self.mesh.bsp_tree()   # Mesh::bsp_tree, mesh.rs:229-231 (depth 20, leaf 4)
-                self.ctx.upload_bsp(self.bsp)
+                if self.device_build:
+                    self.ctx.build_bsp_device(20, 4)
+                else:
+                    self.bsp = self.mesh.bsp_tree()   # Mesh::bsp_tree, mesh.rs:229-231 (depth 20, leaf 4)
+                    self.ctx.upload_bsp(self.bsp)
             else:
-                self.bvh = self.mesh.bvh()        # Mesh::bvh, mesh.rs:233-239 (leaf 4)
-                self.ctx.upload_bvh(self.bvh)
+                if self.device_build:
+                    self.ctx.build_bvh_device(4)
+                else:
+                    self.bvh = self.mesh.bvh()        # Mesh::bvh, mesh.rs:233-239 (leaf 4)
+                    self.ctx.upload_bvh(self.bvh)
         self.ctx.set_environment(self.env)
+        self.ctx.set_environment_map(None)
+        tex = self._background(scene)
+        if tex is not None:
+            self.ctx.set_environment_map(tex)
         npx = self.width * self.height
         self.accum = self.ctx.alloc(npx * 16)
         self.accum.zero()

@@ -289,6 +289,13 @@ int rt_download_bvh(rt_ctx* ctx, rt_gpu_node* nodes, uint32_t cap_nodes, uint32_
  * equirectangular hdri0 texture, res/shaders/w9e1.wgsl:232-241). Default (1,1,1). */
 int rt_set_environment(rt_ctx* ctx, const float rgb[3]);
 
+/* The hdri0 equirectangular background of the W9E1 scenes (src/scenes.rs
+ * background_hdri; src/bindings/texture.rs: Rgba8Unorm, image.to_rgba8()):
+ * width x height RGBA8 texels, row 0 at the top (v = 0).  Sampled by
+ * environment_map (w9e1.wgsl:232-239) as include/rt_detmath.h pins it.
+ * NULL removes it (the constant of rt_set_environment applies again). */
+int rt_set_environment_map(rt_ctx* ctx, const uint8_t* rgba8, uint32_t width, uint32_t height);
+
 /* ---- render (replaces RenderState::render, src/render_state.rs:483-561) -- */
 
 /* Trace `spp` progressive iterations first_iter .. first_iter+spp-1 for every

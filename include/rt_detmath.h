@@ -140,4 +140,77 @@ RT_HD float rt_det_acosf(float x)
     return RT_DET_PIO2F - rt_det__asin_small(x);  /* NaN propagates */
 }
 
+/* atan on |x| <= tan(pi/8) after the Cephes atanf reduction */
+RT_HD float rt_det_atanf(float x)
+{
+    int neg = 0;
+    if (x < 0.0f) {
+        neg = 1;
+        x = -x;
+    }
+    float y0 = 0.0f;
+    if (x > 2.414213562373095f) {            /* tan(3pi/8) */
+        y0 = RT_DET_PIO2F;
+        x = -1.0f / x;
+    } else if (x > 0.4142135623730950f) {    /* tan(pi/8) */
+        y0 = 0.78539816339744830962f;
+        x = (x - 1.0f) / (x + 1.0f);
+    }
+    float z = x * x;
+    float y = (((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z - 3.33329491539e-1f) * z * x
+              + x;
+    y = y0 + y;
+    return neg ? -y : y;   /* NaN propagates */
+}
+
+/* WGSL atan2(y, x); pinned choices where IEEE atan2 distinguishes signed
+ * zeros: atan2(+-0, x < 0) = +pi, atan2(+-0, +-0) = 0. */
+RT_HD float rt_det_atan2f(float y, float x)
+{
+    if (x == 0.0f) {
+        if (y > 0.0f) return RT_DET_PIO2F;
+        if (y < 0.0f) return -RT_DET_PIO2F;
+        return y == y ? 0.0f : y;
+    }
+    float z = rt_det_atanf(y / x);
+    if (x < 0.0f) z = (y < 0.0f) ? z - RT_DET_PIF : z + RT_DET_PIF;
+    return z;
+}
+
+/* environment_map (res/shaders/w9e1.wgsl:232-239) on an RGBA8 (Rgba8Unorm)
+ * equirectangular texture of w x h texels, row 0 at v = 0: the direction's
+ * (u, 1 - v) sampled with the hdri0 sampler's magnification filter --
+ * bilinear, ClampToEdge (src/bindings/texture.rs:134-141).  Pinned choices:
+ * textureSample's LOD comes from fragment-quad derivatives inside the
+ * bounce loop's non-uniform control flow (implementation-defined), so the
+ * magnification (Linear) filter is used for every lookup; texel weights and
+ * the unorm conversion c/255 are f32, evaluated as written here. */
+RT_HD float rt_det__unorm8(unsigned int c) { return (float)c / 255.0f; }
+RT_HD void rt_det_env_sample(const unsigned int* tex, unsigned int w, unsigned int h, float dx, float dy, float dz,
+                             float* rgb)
+{
+    const float u = 0.5f * (1.0f + (1.0f / RT_DET_PIF) * rt_det_atan2f(dx, -dz));
+    const float v = 1.0f / RT_DET_PIF * rt_det_acosf(-dy);
+    const float s = u, t = 1.0f - v;
+    float x = s * (float)w - 0.5f, y = t * (float)h - 0.5f;
+    x = x == x ? x : 0.0f;   /* NaN direction: texel 0 (pinned) */
+    y = y == y ? y : 0.0f;
+    const float fx = __builtin_floorf(x), fy = __builtin_floorf(y);
+    const float a = x - fx, b = y - fy;
+    int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    const int wm = (int)w - 1, hm = (int)h - 1;
+    x0 = x0 < 0 ? 0 : (x0 > wm ? wm : x0);
+    x1 = x1 < 0 ? 0 : (x1 > wm ? wm : x1);
+    y0 = y0 < 0 ? 0 : (y0 > hm ? hm : y0);
+    y1 = y1 < 0 ? 0 : (y1 > hm ? hm : y1);
+    const unsigned int t00 = tex[(unsigned int)y0 * w + (unsigned int)x0], t10 = tex[(unsigned int)y0 * w + (unsigned int)x1];
+    const unsigned int t01 = tex[(unsigned int)y1 * w + (unsigned int)x0], t11 = tex[(unsigned int)y1 * w + (unsigned int)x1];
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    for (int c = 0; c < 3; c++) {
+        const unsigned int sh = 8u * (unsigned int)c;
+        rgb[c] = rt_det__unorm8((t00 >> sh) & 255u) * w00 + rt_det__unorm8((t10 >> sh) & 255u) * w10 +
+                 rt_det__unorm8((t01 >> sh) & 255u) * w01 + rt_det__unorm8((t11 >> sh) & 255u) * w11;
+    }
+}
+
 #endif /* RT02562_DETMATH_H */

@@ -70,6 +70,8 @@ typedef struct or_scene {
     const uint32_t* bvh_ids;
     uint32_t bvh_nids;
     float env[3];              /* constant environment for W9E1 escape */
+    const uint32_t* env_tex;   /* RGBA8 equirectangular hdri0 (NULL: the constant) */
+    uint32_t env_w, env_h;
 } or_scene;
 
 typedef struct or_counts {

@@ -474,7 +474,16 @@ static void sample_path(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t
             if (i == 0) *prim = h.tri;
             result = add(result, w9 ? shade_w9e1(C, &r, &h, &t) : shade_w7e3(C, &r, &h, &t));
         } else {
-            if (w9) result = add(result, mul(load3(C->s->env), h.factor));   /* environment_map(dir)*factor */
+            if (w9) {   /* environment_map(r.direction) * hit.factor, w9e1.wgsl:264-265 */
+                v3 e = load3(C->s->env);
+                if (C->s->env_tex) {
+                    float rgb[3];
+                    rt_det_env_sample(C->s->env_tex, C->s->env_w, C->s->env_h, r.direction.x, r.direction.y,
+                                      r.direction.z, rgb);
+                    e = V(rgb[0], rgb[1], rgb[2]);
+                }
+                result = add(result, mul(e, h.factor));
+            }
             /* W7E3: + BACKGROUND_COLOR (0,0,0) */
             else result = add(result, V(0, 0, 0));
             break;

@@ -42,7 +42,7 @@ class Scene(C.Structure):
                 ("ids", u32p), ("nids", C.c_uint32), ("max_depth", C.c_uint32),
                 ("bvh_nodes", C.POINTER(GpuNode)), ("bvh_nnodes", C.c_uint32),
                 ("bvh_ids", u32p), ("bvh_nids", C.c_uint32),
-                ("env", C.c_float * 3)]
+                ("env", C.c_float * 3), ("env_tex", u32p), ("env_w", C.c_uint32), ("env_h", C.c_uint32)]
 
 
 COUNT_FIELDS = ["samples", "primary", "shadow", "bounce", "node_interior", "node_leaf", "bvh_pops",
@@ -218,8 +218,10 @@ def make_uniform(eye, target, up, constant, width, height, selection1=0, subdiv=
 class SceneRef:
     """Keeps numpy arrays alive behind an or_scene."""
 
-    def __init__(self, mesh, bsp=None, bvh=None, env=(1.0, 1.0, 1.0)):
+    def __init__(self, mesh, bsp=None, bvh=None, env=(1.0, 1.0, 1.0), env_tex=None):
+        """env_tex: RGBA8 equirectangular texture as uint8[h, w, 4] (or None)."""
         self.mesh, self.bsp, self.bvh = mesh, bsp, bvh
+        self.env_tex = None if env_tex is None else np.ascontiguousarray(env_tex, dtype=np.uint8).view(np.uint32)
         s = Scene()
         if mesh is not None:
             s.pos = mesh.pos.ctypes.data_as(f32p)
@@ -245,6 +247,9 @@ class SceneRef:
             s.bvh_ids = bvh.tri_ids.ctypes.data_as(u32p)
             s.bvh_nids = bvh.tri_ids.shape[0]
         s.env[:] = list(env)
+        if self.env_tex is not None:
+            s.env_tex = self.env_tex.ctypes.data_as(u32p)
+            s.env_h, s.env_w = self.env_tex.shape[0], self.env_tex.shape[1]
         self.s = s
 
 

@@ -210,3 +210,39 @@ def test_detail_counters_match_oracle(rt, cornell_bsp):
     check(g, o)
     for k in ("node_interior", "node_leaf", "ids_read", "tri_tests", "tri_accepts"):
         assert g[2][k] == o[2][k], (k, g[2][k], o[2][k])
+
+
+def _envmap_scene(rt, tex, mesh):
+    s = Scene(rt, mesh, "BSP")
+    s.ctx.set_environment_map(tex)
+    s.oscene = s.oscene.__class__(s.om, s.obsp, s.obvh, s.env, env_tex=tex)
+    return s
+
+
+@pytest.mark.parametrize("spp", [1, 3])
+def test_w9e1_environment_texture_synthetic(rt, spp):
+    # hdri0 sampling (w9e1.wgsl:232-239) on an odd-sized random RGBA8 texture
+    rng = np.random.default_rng(11)
+    tex = rng.integers(0, 256, size=(19, 37, 4), dtype=np.uint8)
+    s = _envmap_scene(rt, tex, rt.Mesh.synth_bunny())
+    region = (704, 412, 256, 96)
+    g = s.render_gpu("W9E1", BUNNY_CAM, 1920, 1080, region, 0, spp)
+    o = s.render_oracle("W9E1", BUNNY_CAM, 1920, 1080, region, 0, spp)
+    check(g, o)
+
+
+def test_w9e1_teapot_campus_scene(rt):
+    # scenes.rs "W9 E1 Teapot": teapot.obj, utah teapot camera, 800x450, the
+    # luxo_pxr_campus.jpg background (decoded with PIL: texel values unpinned,
+    # identical on both sides here)
+    import os
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "assets", "textures",
+                        "luxo_pxr_campus.jpg")
+    tex = rt.load_texture_rgba8(path)
+    assert tex.shape == (2000, 4000, 4)
+    s = _envmap_scene(rt, tex, rt.Mesh.from_obj(model("teapot.obj")))
+    region = (0, 180, 800, 40)   # teapot and background
+    g = s.render_gpu("W9E1", TEAPOT_CAM, 800, 450, region, 0, 2)
+    o = s.render_oracle("W9E1", TEAPOT_CAM, 800, 450, region, 0, 2)
+    check(g, o)
+    assert (g[1] != 0xFFFFFFFF).any() and (g[1] == 0xFFFFFFFF).any()
