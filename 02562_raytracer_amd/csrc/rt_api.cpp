@@ -95,6 +95,7 @@ struct rt_ctx {
     DevBuf env_tex;   // RGBA8 equirectangular hdri0 (rt_set_environment_map)
     uint32_t env_w = 0, env_h = 0;
     DevBuf work, counters;
+    DevBuf bvh_deep;   // BVH stack entries beyond the kernels' LDS share
     rt_ray_counts last;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // RT_OPT_KERNEL_TIMING: event pairs around traversal-kernel launches (pool reused after reset)
@@ -822,6 +823,11 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     L.env_w = c->env_w;
     L.env_h = c->env_h;
     L.work_counter = c->work.as<uint32_t>();
+    if (trav == RT_TRAVERSE_BVH) {
+        const size_t need = rtk::bvh_deep_bytes(c->num_cus, c->waves_per_cu);
+        if (c->bvh_deep.n < need) HIPCHK(c, c->bvh_deep.alloc(need));
+        L.bvh_deep = c->bvh_deep.as<uint32_t>();
+    }
     L.shade_threshold = (uint32_t)c->shade_threshold;
     L.min_half_lanes = c->min_half_lanes;
     L.counters = c->counters.as<unsigned long long>();

@@ -68,11 +68,14 @@ struct DevLaunch {
     uint32_t* ids;
     uint32_t* work_counter;       // zeroed before launch
     unsigned long long* counters; // 32 x u64, zeroed before launch (rt_ray_counts order)
+    uint32_t* bvh_deep;           // BVH stack entries beyond the LDS share: (50 - K) x grid lanes
 };
 
 // Launch the kernel for (mode, trav); detail = counting instantiation.
 int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traverse trav, bool detail,
                   int num_cus, int waves_per_cu, hipStream_t stream);
+// bytes of the deep BVH stack for a grid of at most num_cus x waves_per_cu waves
+size_t bvh_deep_bytes(int num_cus, int waves_per_cu);
 
 // Progressive average of one pass's per-iteration samples into accum/ids (after k_path).
 int launch_fold(const DevLaunch& l, hipStream_t stream);

@@ -440,6 +440,27 @@ __device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, co
     return !(t0 > t1);
 }
 
+// BVH stack split: entries [0, K) in LDS ([slot][thread], 4 B), entries [K, 50)
+// in a per-lane global region ([slot - K][lane] across the grid) -- a walk
+// deeper than K is rare, and the LDS share drops from 50 to K entries, which
+// lets the BVH kernels run 8 waves/SIMD like the BSP ones.
+#ifndef RT_BVH_LDS_ENTRIES
+#define RT_BVH_LDS_ENTRIES 16
+#endif
+struct BvhDeep {
+    uint32_t* p;        // this lane's first deep entry (entry j at p[j * stride])
+    uint32_t stride;    // lanes in the grid
+};
+__device__ __forceinline__ void bvh_st(uint32_t* stk, const BvhDeep& dp, uint32_t i, uint32_t v)
+{
+    if (i < RT_BVH_LDS_ENTRIES) stk[i * 256u] = v;
+    else dp.p[(size_t)(i - RT_BVH_LDS_ENTRIES) * dp.stride] = v;
+}
+__device__ __forceinline__ uint32_t bvh_ld(const uint32_t* stk, const BvhDeep& dp, uint32_t i)
+{
+    return i < RT_BVH_LDS_ENTRIES ? stk[i * 256u] : dp.p[(size_t)(i - RT_BVH_LDS_ENTRIES) * dp.stride];
+}
+
 __device__ __forceinline__ void bvh_init(Trav& t, float tmin, float tmax)
 {
     trav_init(t, tmin, tmax);
@@ -459,8 +480,8 @@ __device__ __forceinline__ void bvh_init(Trav& t, float tmin, float tmax)
 // (the left child is the next record), w1 = 0; leaf w0 = byte offset of its
 // first triangle record, w1 = 48 * n_prims.
 template <bool COUNT>
-__device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const f3 o, const f3 d, const f3 inv,
-                                         bool anyhit, Trav& t, Counters& c)
+__device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const BvhDeep& dp, const f3 o, const f3 d,
+                                         const f3 inv, bool anyhit, Trav& t, Counters& c)
 {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bvh_base, (short)0, (int)S.bvh_bytes, 0x00020000);
@@ -499,13 +520,13 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
             t.leaf_end = w0 + w1;
         }
         if (hit & (w1 == 0u)) {   // interior: push left (cur + 1), then right
-            stk[(t.node < 50u ? t.node : 49u) * 256u] = cur + 32u;
+            bvh_st(stk, dp, t.node < 50u ? t.node : 49u, cur + 32u);
             t.node++;
-            stk[(t.node < 50u ? t.node : 49u) * 256u] = w0;
+            bvh_st(stk, dp, t.node < 50u ? t.node : 49u, w0);
             t.node++;
             t.tos = w0;
         } else if (t.node != 0u) {
-            t.tos = stk[(t.node - 1u < 50u ? t.node - 1u : 49u) * 256u];
+            t.tos = bvh_ld(stk, dp, t.node - 1u < 50u ? t.node - 1u : 49u);
         }
     }
     return (t.leaf_k == t.leaf_end) & ((t.lvl >= 1000u) | (t.node == 0u));
@@ -526,23 +547,24 @@ __device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float
     else trav_init(t, tmin, tmax);
 }
 template <int TRAV, bool COUNT>
-__device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const f3 o, const f3 d, const f3 inv,
-                                          bool anyhit, Trav& t, Counters& c)
+__device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const BvhDeep& dp, const f3 o, const f3 d,
+                                          const f3 inv, bool anyhit, Trav& t, Counters& c)
 {
-    if (TRAV == RT_TRAVERSE_BVH) return bvh_step<COUNT>(S, reinterpret_cast<uint32_t*>(stk), o, d, inv, anyhit, t, c);
+    if (TRAV == RT_TRAVERSE_BVH)
+        return bvh_step<COUNT>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv, anyhit, t, c);
     return bsp_step<COUNT>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
 }
 
 // Whole traversal of one ray (used by the primary-ray kernel).
 template <int TRAV, bool COUNT>
-__device__ __forceinline__ bool trace(const DevScene& S, void* stk, const f3 o, const f3 d, float tmin, float tmax,
-                                      bool anyhit, TraceOut& out, Counters& c)
+__device__ __forceinline__ bool trace(const DevScene& S, void* stk, const BvhDeep& dp, const f3 o, const f3 d,
+                                      float tmin, float tmax, bool anyhit, TraceOut& out, Counters& c)
 {
     Trav t;
     trav_start<TRAV>(t, stk, tmin, tmax);
     const f3 inv = trav_inv<TRAV>(d);
     for (uint32_t guard = 0; guard < (1u << 24); guard++)
-        if (trav_step<TRAV, COUNT>(S, stk, o, d, inv, anyhit, t, c)) break;
+        if (trav_step<TRAV, COUNT>(S, stk, dp, o, d, inv, anyhit, t, c)) break;
     out = trav_out(t);
     return t.found;
 }
@@ -662,15 +684,26 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 // registers except the hit record of an accept, and the spills sit in the
 // shading code).  Measured at 256 spp: 5 waves 2744, 6: 2897, 7: 3029,
 // 8: 3084 Mrays/s.
+#ifndef RT_ENV_TEX
+#define RT_ENV_TEX 1
+#endif
+// BVH instantiations: 7 waves/SIMD (72 VGPRs) -- measured 3007 Mrays/s vs
+// 2712 at 8 and 2946 at 6 (256 spp, bunny stand-in)
+#ifndef RT_BVH_WAVES_PER_EU
+#define RT_BVH_WAVES_PER_EU 7
+#endif
 #ifndef RT_PATH_WAVES_PER_EU
 #define RT_PATH_WAVES_PER_EU 8
 #endif
 template <int MODE, int TRAV, bool COUNT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PATH_WAVES_PER_EU, 8)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
+    TRAV == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : RT_PATH_WAVES_PER_EU, 8)))
 k_path(DevScene S, DevLaunch L)
 {
     extern __shared__ uint32_t lds_stack[];   // [level][thread], 4 B entries
     void* stk = lds_stack + threadIdx.x;
+    const BvhDeep dp{TRAV == RT_TRAVERSE_BVH ? L.bvh_deep + (size_t)blockIdx.x * 256u + threadIdx.x : nullptr,
+                     gridDim.x * 256u};
     constexpr bool W9 = MODE == RT_MODE_W9E1;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
@@ -757,7 +790,7 @@ k_path(DevScene S, DevLaunch L)
                 go = go && (leafst ? (nl >= KH || nn < KH) : (nn >= KH || nl < KH));
             }
             if (go) {
-                if (trav_step<TRAV, COUNT>(S, stk, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                if (trav_step<TRAV, COUNT>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }
         }
         if (COUNT) {
@@ -836,7 +869,7 @@ k_path(DevScene S, DevLaunch L)
                 } else {
                     // miss: background (w7e3) / environment_map(dir) * factor (w9e1.wgsl:264-265)
                     f3 e = env;
-                    if (W9 && L.env_tex) {
+                    if (RT_ENV_TEX && W9 && L.env_tex) {
                         float rgb[3];
                         rt_det_env_sample(L.env_tex, L.env_w, L.env_h, rd.x, rd.y, rd.z, rgb);
                         e = V(rgb[0], rgb[1], rgb[2]);
@@ -982,6 +1015,8 @@ __global__ void __launch_bounds__(256) k_primary(DevScene S, DevLaunch L, int pr
 {
     extern __shared__ uint32_t lds_stack[];   // [level][thread], 4 B entries
     void* stk = lds_stack + threadIdx.x;
+    const BvhDeep dp{TRAV == RT_TRAVERSE_BVH ? L.bvh_deep + (size_t)blockIdx.x * 256u + threadIdx.x : nullptr,
+                     gridDim.x * 256u};
     const float ETA = 0.00001f;
     const uint32_t lane = threadIdx.x & 63u;
     const Cam cam = make_cam(L);
@@ -1025,7 +1060,7 @@ __global__ void __launch_bounds__(256) k_primary(DevScene S, DevLaunch L, int pr
             TraceOut tr;
             bool hit = false;
             const bool tracing = alive && !pixel_done;
-            if (tracing) hit = trace<TRAV, COUNT>(S, stk, ro, rd, rtmin, rtmax, false, tr, cnt);
+            if (tracing) hit = trace<TRAV, COUNT>(S, stk, dp, ro, rd, rtmin, rtmax, false, tr, cnt);
             if (tracing) {
                 bool sample_done = false;
                 if (hit) {
@@ -1281,6 +1316,11 @@ static int grid_for(int num_cus, int waves_per_cu)
     return blocks > 0 ? blocks : 1;
 }
 
+size_t bvh_deep_bytes(int num_cus, int waves_per_cu)
+{
+    return (size_t)grid_for(num_cus, waves_per_cu) * 256u * (50u - RT_BVH_LDS_ENTRIES) * 4u;
+}
+
 template <int MODE, int TRAV, bool COUNT>
 static void launch_path(const DevScene& s, const DevLaunch& l, int grid, size_t lds, hipStream_t st)
 {
@@ -1295,11 +1335,15 @@ static void launch_primary(const DevScene& s, const DevLaunch& l, int project, i
 int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traverse trav, bool detail, int num_cus,
                   int waves_per_cu, hipStream_t stream)
 {
-    const size_t lds = trav == RT_TRAVERSE_BVH ? (size_t)50 * 256 * 4 : (size_t)(s.bsp_depth ? s.bsp_depth : 1) * 256 * 4;
+    const size_t lds = trav == RT_TRAVERSE_BVH ? (size_t)RT_BVH_LDS_ENTRIES * 256 * 4
+                                               : (size_t)(s.bsp_depth ? s.bsp_depth : 1) * 256 * 4;
     // a persistent grid larger than what fits at once (160 KiB LDS per CU)
     // would only add blocks that start after the queue ran dry
     const int lds_waves = 4 * (int)((160u * 1024u) / (lds ? lds : 1));
-    const int grid = grid_for(num_cus, std::min(waves_per_cu > 0 ? waves_per_cu : 16, std::max(4, lds_waves)));
+    // and by the register budget k_path is fitted to (waves per SIMD x 4 SIMDs)
+    const int reg_waves = 4 * (trav == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : RT_PATH_WAVES_PER_EU);
+    const int grid = grid_for(num_cus, std::min(std::min(waves_per_cu > 0 ? waves_per_cu : 16, reg_waves),
+                                                std::max(4, lds_waves)));
     if (mode == RT_MODE_W1E6) {
         hipLaunchKernelGGL(k_w1e6, dim3(grid), dim3(256), 0, stream, l);
         return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
