@@ -711,6 +711,11 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 #ifndef RT_PATH_WAVES_PER_EU
 #define RT_PATH_WAVES_PER_EU 8
 #endif
+// W9E1 with uniforms.selection1 == 7 (the transparent shader) runs as its own
+// instantiation: its shading code in the default kernel raises the register
+// pressure enough to spill inside the traversal loop.
+constexpr int MODE_W9E1_TRANSPARENT = 100 + RT_MODE_W9E1;
+
 template <int MODE, int TRAV, bool COUNT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     TRAV == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : RT_PATH_WAVES_PER_EU, 8)))
@@ -726,7 +731,8 @@ k_path(DevScene S, DevLaunch L)
                                         : lds_stack + threadIdx.x;
     const BvhDeep dp{TRAV == RT_TRAVERSE_BVH ? L.bvh_deep + (size_t)blockIdx.x * 256u + threadIdx.x : nullptr,
                      gridDim.x * 256u};
-    constexpr bool W9 = MODE == RT_MODE_W9E1;
+    constexpr bool W9 = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT;
+    constexpr bool XT = MODE == MODE_W9E1_TRANSPARENT;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
     const Cam cam = make_cam(L);
@@ -865,11 +871,53 @@ k_path(DevScene S, DevLaunch L)
                         shadow = true;
                         st = ST_TRACE;
                         cnt.v[C_SHADOW]++;
-                    } else if (sel == 2u) {
-                        // mirror (w9e1.wgsl:491-504): reflect, offset origin, emit = true
-                        const f3 n = h.nrm;
-                        rd = sub(rd, muls(n, 2.0f * dot(n, rd)));
-                        ro = add(h.pos, muls(n, ETA));
+                    } else if (sel == 2u || (XT && sel == 7u)) {
+                        f3 n = h.nrm;
+                        bool reflect_ray = true;
+                        if (XT && sel == 7u) {
+                            // transparent (w9e1.wgsl:505-558); hit_record_init: ior1_over_ior2 1.0,
+                            // extinction (1,1,1).  The refracted ray replaces r before the mirror
+                            // branch reflects it (as the shader does).
+                            const f3 w_i = neg(normalize(rd));
+                            const f3 normal = normalize(h.nrm);
+                            const f3 ext = V(1.0f, 1.0f, 1.0f);
+                            f3 out_n;
+                            float ior = 1.0f, cos_i = dot(w_i, normal), absorption = 0.0f;
+                            if (cos_i < 0.0f) {
+                                cos_i = dot(w_i, neg(normal));
+                                out_n = neg(normal);
+                            } else {
+                                ior = 1.0f / ior;
+                                out_n = normal;
+                                const f3 dd = sub(h.pos, ro);
+                                const float sd = rt_det_sqrtf(dot(dd, dd));
+                                const f3 nr = neg(ext);
+                                const f3 tr = V(rt_det_expf(nr.x * sd), rt_det_expf(nr.y * sd), rt_det_expf(nr.z * sd));
+                                absorption = 1.0f - (tr.x + tr.y + tr.z) / 3.0f;
+                            }
+                            const float cos_t2 = (1.0f - (ior * ior) * (1.0f - cos_i * cos_i));
+                            float refl = 1.0f;
+                            if (!(cos_t2 < 0.0f)) {   // fresnel_r, w9e1.wgsl:191-201
+                                const float ct = rt_det_sqrtf(cos_t2);
+                                const float ii = ior * cos_i, tt = 1.0f * ct, ti = 1.0f * cos_i, it2 = ior * ct;
+                                const float r1 = (ii - tt) / (ii + tt), r2 = (ti - it2) / (ti + it2);
+                                refl = 0.5f * (r1 * r1 + r2 * r2);
+                            }
+                            const f3 tangent = sub(muls(out_n, cos_i), w_i);
+                            rd = sub(muls(tangent, ior), muls(normalize(out_n), rt_det_sqrtf(cos_t2)));
+                            ro = h.pos;
+                            reflect_ray = rnd(rng) < refl;
+                            if (reflect_ray) {
+                                n = out_n;
+                            } else if (rnd(rng) < absorption) {
+                                fac = mul(fac, divs(ext, absorption));
+                            }
+                        }
+                        if (reflect_ray) {
+                            // mirror (w9e1.wgsl:491-504): reflect, offset origin
+                            rd = sub(rd, muls(n, 2.0f * dot(n, rd)));
+                            ro = add(h.pos, muls(n, ETA));
+                        }
                         emit = true;
                         if (bounce + 1u < 50u) {
                             bounce++;
@@ -1385,10 +1433,17 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
                     : launch_path<RT_MODE_W7E3, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         break;
     case RT_MODE_W9E1:
-        if (bvh) detail ? launch_path<RT_MODE_W9E1, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
-                        : launch_path<RT_MODE_W9E1, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
-        else detail ? launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
-                    : launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        if (l.u.selection1 == 7u) {
+            if (bvh) detail ? launch_path<MODE_W9E1_TRANSPARENT, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                            : launch_path<MODE_W9E1_TRANSPARENT, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+            else detail ? launch_path<MODE_W9E1_TRANSPARENT, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                        : launch_path<MODE_W9E1_TRANSPARENT, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        } else {
+            if (bvh) detail ? launch_path<RT_MODE_W9E1, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                            : launch_path<RT_MODE_W9E1, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+            else detail ? launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                        : launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        }
         break;
     case RT_MODE_W6E1:
     case RT_MODE_PROJECT: {

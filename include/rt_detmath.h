@@ -140,6 +140,26 @@ RT_HD float rt_det_acosf(float x)
     return RT_DET_PIO2F - rt_det__asin_small(x);  /* NaN propagates */
 }
 
+/* exp: Cephes expf (range reduction by ln 2 in two parts, degree-5
+ * polynomial), scaled by ldexp (exact).  Used by W9E1's transparent shader
+ * (w9e1.wgsl:525, T_r = exp(-rho_t * s)). */
+RT_HD float rt_det_expf(float x)
+{
+    if (x != x) return x;
+    if (x > 88.72283905206835f) return __builtin_inff();
+    if (x < -103.972077083991796f) return 0.0f;
+    const float fx = __builtin_floorf(x * 1.44269504088896341f + 0.5f);
+    x = x - fx * 0.693359375f;
+    x = x - fx * -2.12194440e-4f;
+    const float z = x * x;
+    const float y = ((((( 1.9875691500E-4f * x + 1.3981999507E-3f) * x + 8.3334519073E-3f) * x
+                       + 4.1665795894E-2f) * x + 1.6666665459E-1f) * x + 5.0000001201E-1f) * z + x + 1.0f;
+    const int n = (int)fx;
+    /* 2^n in two exact steps (n in [-150, 128]) */
+    const int n1 = n / 2, n2 = n - n1;
+    return __builtin_ldexpf(__builtin_ldexpf(y, n1), n2);
+}
+
 /* atan on |x| <= tan(pi/8) after the Cephes atanf reduction */
 RT_HD float rt_det_atanf(float x)
 {

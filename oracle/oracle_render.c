@@ -436,6 +436,59 @@ static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
         return muls(add(h->normal, V(1.0f, 1.0f, 1.0f)), 0.5f);
     case 6:
         return add(load3(m->diffuse), load3(m->ambient));
+    case 7: {   /* transparent, w9e1.wgsl:505-558; hit_record_init: ior1_over_ior2 1.0, extinction (1,1,1) */
+        v3 w_i = neg(normalize(r->direction));
+        v3 normal = normalize(h->normal);
+        v3 out_normal;
+        float ior = 1.0f;
+        float cos_i = dot(w_i, normal);
+        float absorption = 0.0f;
+        v3 extinction = V(1.0f, 1.0f, 1.0f);
+        if (cos_i < 0.0f) {
+            cos_i = dot(w_i, neg(normal));
+            out_normal = neg(normal);
+        } else {
+            ior = 1.0f / ior;
+            out_normal = normal;
+            v3 dd = sub(h->position, r->origin);
+            float sd = rt_det_sqrtf(dot(dd, dd));                     /* length() */
+            v3 nr = neg(extinction);
+            v3 tr = V(rt_det_expf(nr.x * sd), rt_det_expf(nr.y * sd), rt_det_expf(nr.z * sd));
+            absorption = 1.0f - (tr.x + tr.y + tr.z) / 3.0f;
+        }
+        float cos_t2 = (1.0f - (ior * ior) * (1.0f - cos_i * cos_i));
+        float refl;
+        if (cos_t2 < 0.0f) {
+            refl = 1.0f;
+        } else {   /* fresnel_r, w9e1.wgsl:191-201 */
+            float ct = rt_det_sqrtf(cos_t2);
+            float ii = ior * cos_i, tt = 1.0f * ct, ti = 1.0f * cos_i, it = ior * ct;
+            float r1 = (ii - tt) / (ii + tt), r2 = (ti - it) / (ti + it);
+            refl = 0.5f * (r1 * r1 + r2 * r2);
+        }
+        v3 tangent = sub(muls(out_normal, cos_i), w_i);
+        v3 w_t = sub(muls(tangent, ior), muls(normalize(out_normal), rt_det_sqrtf(cos_t2)));
+        r->direction = w_t;            /* ray_init(w_t, position) */
+        r->origin = h->position;
+        r->tmax = 5000.0f;
+        r->tmin = ETA;
+        h->has_hit = 0;
+        h->emit = 1;
+        float step = rnd(t);
+        if (step < refl) {             /* mirror(r, hit) with hit.normal = out_normal */
+            h->normal = out_normal;
+            v3 n = h->normal, d = r->direction;
+            v3 rd = sub(d, muls(n, 2.0f * dot(n, d)));
+            r->origin = add(h->position, muls(n, ETA));
+            r->direction = rd;
+            r->tmax = 5000.0f;
+            r->tmin = ETA;
+            return V(0, 0, 0);
+        }
+        float step1 = rnd(t);
+        if (step1 < absorption) h->factor = mul(h->factor, divs(extinction, absorption));
+        return V(0, 0, 0);
+    }
     default:
         return V(0.7f, 0.0f, 0.7f);
     }

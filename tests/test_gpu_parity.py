@@ -127,7 +127,7 @@ def test_axis_aligned_and_tiny_direction_components(rt, gpu, mode, trav):
     assert (g[1] != 0xFFFFFFFF).any()
 
 
-@pytest.mark.parametrize("sel", [2, 5, 6, 4])
+@pytest.mark.parametrize("sel", [2, 5, 6, 4, 7])
 def test_shader_selection(rt, gpu, sel):
     # uniforms.selection1 switch of shade(): mirror, normal, base colour, default (error colour)
     s = Scene(rt, rt.Mesh.from_obj(model("teapot.obj")), "BSP")
