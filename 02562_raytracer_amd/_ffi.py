@@ -131,6 +131,7 @@ SIGNATURES = {
     "rt_memset_device": (C.c_int, [vp, vp, C.c_int, C.c_size_t]),
     "rt_timer_start": (C.c_int, [vp]),
     "rt_timer_stop": (C.c_int, [vp, f32p]),
+    "rt_frame_rgba8": (C.c_int, [vp, vp, C.c_uint32, vp]),
     "rt_kernel_time": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), u32p]),
     "rt_build_bvh_device": (C.c_int, [vp, C.c_uint32, C.POINTER(BvhBuildTimes)]),
     "rt_build_bsp_device": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(BspBuildTimes)]),

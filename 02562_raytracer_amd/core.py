@@ -395,6 +395,10 @@ class Context:
         self._chk(F.lib().rt_timer_stop(self._h, C.byref(ms)))
         return ms.value
 
+    def frame_rgba8(self, accum_ptr, npix, out_ptr):
+        """Display transform of npix accumulated pixels into 8-bit sRGB RGBA (device pointers)."""
+        self._chk(F.lib().rt_frame_rgba8(self._h, C.c_void_p(accum_ptr), npix, C.c_void_p(out_ptr)))
+
     def kernel_time(self, reset=True):
         """(summed ms, launches) of the traversal-kernel launches timed since the
         last reset (RT_OPT_KERNEL_TIMING must be on); synchronizes."""

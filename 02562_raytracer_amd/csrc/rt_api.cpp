@@ -96,6 +96,7 @@ struct rt_ctx {
     uint32_t env_w = 0, env_h = 0;
     DevBuf work, counters;
     DevBuf bvh_deep;   // BVH stack entries beyond the kernels' LDS share
+    DevBuf srgb_thr;   // rt_frame_rgba8's 8-bit sRGB code thresholds
     rt_ray_counts last;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     // RT_OPT_KERNEL_TIMING: event pairs around traversal-kernel launches (pool reused after reset)
@@ -927,6 +928,43 @@ int rt_render_tiles(rt_ctx* c, rt_mode mode, rt_traverse trav, const rt_tileset*
     L.accum = reinterpret_cast<float4*>(accum);
     L.ids = ids;
     return render_common(c, mode, trav, L, counts);
+}
+
+// The 255 thresholds of 8-bit sRGB codes: code k+1 starts where
+// 255 * oetf(v) reaches k + 0.5 (oetf inverted in double, rounded up to the
+// first float whose code is k + 1).
+static void srgb_code_thresholds(float* t)
+{
+    for (int k = 0; k < 255; k++) {
+        const double e = (k + 0.5) / 255.0;   // encoded value at the rounding midpoint
+        const double v = e <= 0.04045 ? e / 12.92 : std::pow((e + 0.055) / 1.055, 2.4);
+        float f = (float)v;
+        auto code = [](float x) {
+            const double xd = x;
+            const double enc = xd <= 0.0031308 ? 12.92 * xd : 1.055 * std::pow(xd, 1.0 / 2.4) - 0.055;
+            return (int)std::floor(enc * 255.0 + 0.5);
+        };
+        while (code(f) > k) f = std::nextafter(f, 0.0f);
+        while (code(f) <= k) f = std::nextafter(f, 2.0f);
+        t[k] = f;
+    }
+}
+
+int rt_frame_rgba8(rt_ctx* c, const float* accum_rgba32f, uint32_t npix, uint8_t* frame_rgba8)
+{
+    if (!c || (!accum_rgba32f && npix) || (!frame_rgba8 && npix)) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    if (!c->srgb_thr.p) {
+        float t[256];
+        srgb_code_thresholds(t);
+        t[255] = 0.0f;
+        if (int r = upload(c, c->srgb_thr, t, sizeof t)) return r;
+    }
+    if (npix == 0) return RT_OK;
+    if (rtk::launch_frame(reinterpret_cast<const float4*>(accum_rgba32f), npix, c->srgb_thr.as<float>(),
+                          reinterpret_cast<uchar4*>(frame_rgba8), c->stream))
+        return fail(c, RT_E_DEVICE, "rt_frame_rgba8: launch failed");
+    return RT_OK;
 }
 
 int rt_unpack_tiles(rt_ctx* c, uint32_t width, uint32_t height, uint32_t nranks, const float* packed_accum,

@@ -80,6 +80,9 @@ size_t bvh_deep_bytes(int num_cus, int waves_per_cu);
 // Progressive average of one pass's per-iteration samples into accum/ids (after k_path).
 int launch_fold(const DevLaunch& l, hipStream_t stream);
 
+// display frame: RGBA32F accum -> 8-bit sRGB (thr: 255 device floats, srgb_code_thresholds)
+int launch_frame(const float4* accum, uint32_t npix, const float* thr, uchar4* out, hipStream_t stream);
+
 int launch_unpack(uint32_t width, uint32_t height, uint32_t nranks, uint32_t local_tiles,
                   const float4* packed_accum, const uint32_t* packed_ids, float4* frame_accum,
                   uint32_t* frame_ids, hipStream_t stream);

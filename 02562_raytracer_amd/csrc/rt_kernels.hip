@@ -1332,6 +1332,48 @@ __global__ void __launch_bounds__(256) k_unpack(uint32_t W, uint32_t H, uint32_t
     }
 }
 
+// ------------------------------------------------------------------ display frame
+// fs_main's frame output (w7e3.wgsl:261-271, w9e1.wgsl:272-283):
+// saturate(pow(accum, 1.5)), written to the sRGB surface (render_state.rs:
+// 108-115, is_srgb()), i.e. encoded to 8-bit sRGB by the presentation engine.
+// Pinned choices (the display path is outside the parity contract, SURVEY.md
+// 8(a) a13): pow(x, 1.5) = x * sqrt(x); the 8-bit sRGB code is the exact
+// rounding of 255 * srgb_oetf(v), found by counting the 255 code thresholds
+// (computed on the host in double precision) that v reaches.
+__global__ void __launch_bounds__(256) k_frame(const float4* accum, uint32_t npix, const float* thr, uchar4* out)
+{
+    __shared__ float t[256];
+    t[threadIdx.x] = threadIdx.x < 255u ? thr[threadIdx.x] : 3.0e38f;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < npix; i += gridDim.x * 256u) {
+        const float4 a = accum[i];
+        const float c[3] = {a.x, a.y, a.z};
+        unsigned char q[3];
+        for (int k = 0; k < 3; k++) {
+            const float x = c[k] > 0.0f ? c[k] : 0.0f;
+            float v = x * rt_det_sqrtf(x);            // pow(x, 1.5)
+            v = v < 1.0f ? v : 1.0f;                  // saturate
+            uint32_t lo = 0, hi = 255;                // code = #thresholds <= v
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (t[mid] <= v) lo = mid + 1u;
+                else hi = mid;
+            }
+            q[k] = (unsigned char)lo;
+        }
+        out[i] = make_uchar4(q[0], q[1], q[2], 255);
+    }
+}
+
+int launch_frame(const float4* accum, uint32_t npix, const float* thr, uchar4* out, hipStream_t stream)
+{
+    uint64_t blocks = ((uint64_t)npix + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_frame, dim3((uint32_t)blocks), dim3(256), 0, stream, accum, npix, thr, out);
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+
 // ------------------------------------------------------------------ math self test
 __host__ __device__ inline void math_eval(float x, float* o)
 {

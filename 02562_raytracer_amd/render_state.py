@@ -124,6 +124,21 @@ class RenderState:
     def hit_ids(self):
         return self.ids.to_numpy(np.uint32, (self.height, self.width))
 
+    def frame_rgba8(self):
+        """The displayed frame as the sRGB surface holds it: uint8 [H, W, 4]
+        (rt_frame_rgba8, on the device)."""
+        npx = self.width * self.height
+        out = self.ctx.alloc(npx * 4)
+        self.ctx.frame_rgba8(self.accum.ptr, npx, out.ptr)
+        img = out.to_numpy(np.uint8, (self.height, self.width, 4))
+        out.free()
+        return img
+
+    def save_png(self, path):
+        """Write the displayed frame (PIL)."""
+        from PIL import Image
+        Image.fromarray(self.frame_rgba8(), "RGBA").save(path)
+
     @staticmethod
     def display(accum):
         """fs_main's frame output: saturate(pow(accum, 1.5)) (w7e3.wgsl:265)."""

@@ -332,6 +332,13 @@ int rt_render_tiles(rt_ctx* ctx, rt_mode mode, rt_traverse trav, const rt_tilese
  * rounded up, so packed buffers have one size: ceil(ntiles / nranks)). */
 uint32_t rt_tileset_local_tiles(uint32_t width, uint32_t height, uint32_t nranks);
 
+/* The displayed frame of fs_main (w7e3.wgsl:261-271): saturate(pow(accum, 1.5))
+ * as the sRGB surface stores it (render_state.rs:108-115), 8-bit RGBA, for
+ * npix pixels; device pointers, asynchronous on the context stream.  The
+ * pow and the sRGB rounding are pinned here (the display path is outside
+ * the parity contract). */
+int rt_frame_rgba8(rt_ctx* ctx, const float* accum_rgba32f, uint32_t npix, uint8_t* frame_rgba8);
+
 /* Scatter gathered packed buffers (nranks x local_tiles x 64 px, rank-major as
  * produced by an all-gather) into a row-major W x H frame, on the context's
  * stream.  Either pair of pointers may be NULL. */

@@ -246,3 +246,20 @@ def test_w9e1_teapot_campus_scene(rt):
     o = s.render_oracle("W9E1", TEAPOT_CAM, 800, 450, region, 0, 2)
     check(g, o)
     assert (g[1] != 0xFFFFFFFF).any() and (g[1] == 0xFFFFFFFF).any()
+
+
+def test_display_frame_rgba8(rt):
+    # fs_main's frame output through rt_frame_rgba8: saturate(pow(accum, 1.5)) in
+    # 8-bit sRGB, checked against a float64 host evaluation of the same pinned
+    # definition (exact 8-bit rounding away from the code thresholds)
+    rs = rt.RenderState(rt.find_scene("W7 E3 Cornell Box"), resolution=(64, 48))
+    rs.render(spp=4)
+    acc = rs.frame().astype(np.float64)
+    img = rs.frame_rgba8()
+    v = np.clip(np.maximum(acc[..., :3], 0) ** 1.5, 0, 1)
+    enc = np.where(v <= 0.0031308, 12.92 * v, 1.055 * v ** (1 / 2.4) - 0.055)
+    ref = np.floor(enc * 255 + 0.5)
+    near = np.abs(enc * 255 - np.floor(enc * 255) - 0.5) < 1e-3   # float rounding of pow/sqrt may flip these
+    assert np.all((img[..., :3] == ref) | near)
+    assert np.all(img[..., 3] == 255)
+    rs.ctx.close()
