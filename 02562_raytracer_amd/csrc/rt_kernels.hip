@@ -711,6 +711,121 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 #ifndef RT_PATH_WAVES_PER_EU
 #define RT_PATH_WAVES_PER_EU 8
 #endif
+// intersect_sphere (w1e6.wgsl / w8e1.wgsl:352-376): closest root in [tmin, tmax]
+__device__ __forceinline__ bool w1_sphere(f3 o, f3 w, float tmin, float& tmax, f3 center, float radius, f3& pos,
+                                          f3& nrm)
+{
+    const f3 oc = sub(o, center);
+    const float a = dot(w, w);
+    const float b2 = dot(oc, w);
+    const float c = dot(oc, oc) - radius * radius;
+    const float disc = b2 * b2 - a * c;
+    if (disc < 0.0f) return false;
+    const float ds = rt_det_sqrtf(disc);
+    float root = (-b2 - ds) / a;
+    if (root < tmin || root > tmax) {
+        root = (-b2 + ds) / a;
+        if (root < tmin || root > tmax) return false;
+    }
+    tmax = root;
+    pos = add(o, muls(w, root));
+    nrm = normalize(sub(pos, center));
+    return true;
+}
+// The two balls of intersect_scene_bsp (w8e1.wgsl:244-262), in its order: the
+// mirror ball, then the glass ball on the interval the first leaves.  id 0:
+// none, 1: mirror, 2: transparent (ior1_over_ior2 1.5).  The kernel tests them
+// when a ray starts (their nearest hit bounds the mesh walk, as r.tmax does in
+// the shader) and again when a ray that found no triangle is shaded.
+struct W8Ball {
+    uint32_t id;
+    float t;
+    f3 pos, nrm;
+};
+__device__ __forceinline__ W8Ball w8_balls(f3 o, f3 w, float tmin, float tmax)
+{
+    W8Ball b;
+    b.id = 0;
+    b.t = tmax;
+    b.pos = b.nrm = V(0, 0, 0);
+    if (w1_sphere(o, w, tmin, b.t, V(420.0f, 90.0f, 370.0f), 90.0f, b.pos, b.nrm)) b.id = 1;
+    if (w1_sphere(o, w, tmin, b.t, V(130.0f, 90.0f, 250.0f), 90.0f, b.pos, b.nrm)) b.id = 2;
+    return b;
+}
+
+// Shading of a ball hit (shade(), w8e1.wgsl:379-404): mirror (id 1,
+// w8e1.wgsl:437-445 / w8e2.wgsl:509-522) or transparent (id 2,
+// w8e1.wgsl:447-490 / w8e2.wgsl:524-569 / w8e3.wgsl: absorption on exit).
+// Replaces the ray (ro, rd) and updates factor/emit; adds what the shader
+// returns (0, or error_shader()) to res.  Returns true when the sample goes on
+// with the new ray.  Under total internal reflection w_t carries sqrt of a
+// negative number (NaN), as in the shader; the walks and the oracle follow
+// IEEE comparison semantics for it.
+template <int MODE>
+__device__ __forceinline__ bool w8_ball_shade(const W8Ball& b, f3& ro, f3& rd, f3& fac, bool& emit, f3& res,
+                                              uint32_t& rng, float ETA)
+{
+    constexpr bool E1 = MODE == RT_MODE_W8E1, E2 = MODE == RT_MODE_W8E2, E3 = MODE == RT_MODE_W8E3;
+    f3 n = b.nrm;
+    bool go = true, reflect_ray = true;
+    if (b.id == 2u) {
+        const f3 w_i = neg(normalize(rd));
+        const f3 normal = normalize(n);
+        f3 out_n;
+        float ior = 1.5f, cos_i = dot(w_i, normal), tp = 0.0f;
+        const bool entering = cos_i < 0.0f;
+        f3 T_r = V(1.0f, 1.0f, 1.0f);
+        if (entering) {
+            cos_i = dot(w_i, neg(normal));
+            out_n = neg(normal);
+        } else {
+            ior = 1.0f / ior;
+            out_n = normal;
+            if (E3) {   // T_r = exp(-rho_t * s), s = length(position - origin) / 100
+                const f3 dd = sub(b.pos, ro);
+                const float sd = rt_det_sqrtf(dot(dd, dd)) / 100.0f;
+                const f3 nr = neg(V(0.5f, 0.2f, 0.2f));
+                T_r = V(rt_det_expf(nr.x * sd), rt_det_expf(nr.y * sd), rt_det_expf(nr.z * sd));
+                tp = (T_r.x + T_r.y + T_r.z) / 3.0f;
+                if (tp < 0.0f || tp > 1.0f) {
+                    res = add(res, V(0.7f, 0.0f, 0.7f));   // error_shader; has_hit ends the sample
+                    return false;
+                }
+            }
+        }
+        const float cos_t2 = (1.0f - (ior * ior) * (1.0f - cos_i * cos_i));
+        float refl = 1.0f;
+        if (!(cos_t2 < 0.0f)) {   // fresnel_r, w8e2.wgsl:202-212
+            const float ct = rt_det_sqrtf(cos_t2);
+            const float ii = ior * cos_i, tt = 1.0f * ct, ti = 1.0f * cos_i, it2 = ior * ct;
+            const float r1 = (ii - tt) / (ii + tt), r2 = (ti - it2) / (ti + it2);
+            refl = 0.5f * (r1 * r1 + r2 * r2);
+            if (E1) refl = rt_satf(refl);
+        }
+        const f3 tangent = sub(muls(out_n, cos_i), w_i);
+        rd = sub(muls(tangent, ior), muls(E1 ? out_n : normalize(out_n), rt_det_sqrtf(cos_t2)));
+        ro = b.pos;
+        if (!E1) emit = true;
+        const float step = rnd(rng);
+        reflect_ray = step < refl;
+        if (reflect_ray) {
+            n = out_n;
+        } else if (E2) {
+            fac = divs(fac, 1.0f - refl);
+        } else if (E3 && !entering) {
+            if (step < refl + tp) fac = divs(mul(fac, T_r), refl + tp);
+            else go = false;   // absorbed
+        }
+    }
+    if (reflect_ray) {
+        rd = sub(rd, muls(n, 2.0f * dot(n, rd)));   // reflect
+        ro = E1 ? b.pos : add(b.pos, muls(n, ETA));
+        if (!E1) emit = true;
+    }
+    res = add(res, V(0, 0, 0));   // result += shade() (= vec3(0)); keeps -0 + 0 semantics
+    return go;
+}
+
 // W9E1 with uniforms.selection1 == 7 (the transparent shader) runs as its own
 // instantiation: its shading code in the default kernel raises the register
 // pressure enough to spill inside the traversal loop.
@@ -733,6 +848,14 @@ k_path(DevScene S, DevLaunch L)
                      gridDim.x * 256u};
     constexpr bool W9 = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT;
     constexpr bool XT = MODE == MODE_W9E1_TRANSPARENT;
+    // W8E1/W8E2/W8E3: the Cornell box with its two analytic balls; W8E1 lights
+    // directly only (10 segments), W8E2/W8E3 path trace with a firefly clamp
+    constexpr bool W8 = MODE == RT_MODE_W8E1 || MODE == RT_MODE_W8E2 || MODE == RT_MODE_W8E3;
+    constexpr bool W8E1 = MODE == RT_MODE_W8E1;
+    constexpr bool W8E3 = MODE == RT_MODE_W8E3;
+    constexpr bool CLAMP = W8 && !W8E1;
+    constexpr bool FAC_AMB = W9 || W8E3;   // ambient = emission * factor
+    constexpr uint32_t MAXD = W8E1 ? 10u : 50u;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
     const Cam cam = make_cam(L);
@@ -778,7 +901,7 @@ k_path(DevScene S, DevLaunch L)
         prim = 0xFFFFFFFFu;
         shadow = false;
         inv = trav_inv<TRAV>(rd);
-        trav_start<TRAV>(tr, stk, ETA, 5000.0f);
+        trav_start<TRAV>(tr, stk, ETA, W8 ? w8_balls(ro, rd, ETA, 5000.0f).t : 5000.0f);
         st = ST_TRACE;
         cnt.v[C_SAMPLES]++;
         cnt.v[C_PRIMARY]++;
@@ -853,13 +976,18 @@ k_path(DevScene S, DevLaunch L)
                         }
                         f3 dv = mul(muls(brdf, rt_satf(dot(h.nrm, Lt.w_i))), Lt.l_i);
                         if (!W9) dv = muls(dv, (float)light_tris);
-                        const f3 amb = emit ? (W9 ? mul(emission, fac) : emission) : V(0, 0, 0);
+                        const f3 amb = emit ? (FAC_AMB ? mul(emission, fac) : emission) : V(0, 0, 0);
                         cu = add(mul(dv, fac), amb);             // not blocked: diffuse*factor + ambient
-                        cb = add(mul(V(0, 0, 0), fac), amb);     // blocked: vec3(0)*factor + ambient
+                        // blocked: vec3(0)*factor + ambient (w8e3.wgsl: vec3(0) + ambient)
+                        cb = add(W8E3 ? V(0, 0, 0) : mul(V(0, 0, 0), fac), amb);
+                        if (CLAMP) {   // min(shade(), firefly_clamp), w8e2.wgsl:265
+                            cu = V(rt_minf(cu.x, 100.0f), rt_minf(cu.y, 100.0f), rt_minf(cu.z, 100.0f));
+                            cb = V(rt_minf(cb.x, 100.0f), rt_minf(cb.y, 100.0f), rt_minf(cb.z, 100.0f));
+                        }
                         fac = mul(fac, muls(brdf, RT_PI_F));
                         const float prob = (brdf.x + brdf.y + brdf.z) / 3.0f;
-                        survive = rnd(rng) < prob;
-                        if (survive && bounce + 1u < 50u) {
+                        survive = !W8E1 && rnd(rng) < prob;   // w8e1.wgsl: direct light only
+                        if (survive && bounce + 1u < MAXD) {
                             ndir = indirect_dir(h.nrm, rng);   // setup_indirect (:472-489)
                             fac = divs(fac, prob);
                         }
@@ -867,10 +995,15 @@ k_path(DevScene S, DevLaunch L)
                         ro = h.pos;
                         rd = Lt.w_i;
                         inv = trav_inv<TRAV>(rd);
-                        trav_start<TRAV>(tr, stk, ETA, Lt.dist - ETA);
                         shadow = true;
                         st = ST_TRACE;
                         cnt.v[C_SHADOW]++;
+                        if (W8 && w8_balls(ro, rd, ETA, Lt.dist - ETA).id != 0u) {
+                            tr.found = true;   // a ball blocks the light: no mesh walk
+                            st = ST_SHADE;
+                        } else {
+                            trav_start<TRAV>(tr, stk, ETA, Lt.dist - ETA);
+                        }
                     } else if (sel == 2u || (XT && sel == 7u)) {
                         f3 n = h.nrm;
                         bool reflect_ray = true;
@@ -937,23 +1070,38 @@ k_path(DevScene S, DevLaunch L)
                         sample_done = true;
                     }
                 } else {
-                    // miss: background (w7e3) / environment_map(dir) * factor (w9e1.wgsl:264-265)
-                    f3 e = env;
-                    if (RT_ENV_TEX && W9 && L.env_tex) {
-                        float rgb[3];
-                        rt_det_env_sample(L.env_tex, L.env_w, L.env_h, rd.x, rd.y, rd.z, rgb);
-                        e = V(rgb[0], rgb[1], rgb[2]);
+                    W8Ball ball;
+                    ball.id = 0u;
+                    if (W8) ball = w8_balls(ro, rd, ETA, 5000.0f);
+                    if (W8 && ball.id != 0u) {
+                        if (w8_ball_shade<MODE>(ball, ro, rd, fac, emit, res, rng, ETA) && bounce + 1u < MAXD) {
+                            bounce++;
+                            inv = trav_inv<TRAV>(rd);
+                            trav_start<TRAV>(tr, stk, ETA, w8_balls(ro, rd, ETA, 5000.0f).t);
+                            st = ST_TRACE;
+                            cnt.v[C_BOUNCE]++;
+                        } else {
+                            sample_done = true;
+                        }
+                    } else {
+                        // miss: background (w7e3, w8e*) / environment_map(dir) * factor (w9e1.wgsl:264-265)
+                        f3 e = env;
+                        if (RT_ENV_TEX && W9 && L.env_tex) {
+                            float rgb[3];
+                            rt_det_env_sample(L.env_tex, L.env_w, L.env_h, rd.x, rd.y, rd.z, rgb);
+                            e = V(rgb[0], rgb[1], rgb[2]);
+                        }
+                        res = add(res, W9 ? mul(e, fac) : (W8E1 ? V(0.1f, 0.3f, 0.6f) : V(0, 0, 0)));
+                        sample_done = true;
                     }
-                    res = add(res, W9 ? mul(e, fac) : V(0, 0, 0));
-                    sample_done = true;
                 }
             } else {
                 // shadow ray finished: rest of lambertian, then the bounce
                 res = add(res, tr.found ? cb : cu);
-                if (survive && bounce + 1u < 50u) {
+                if (survive && bounce + 1u < MAXD) {
                     rd = ndir;   // origin = hit position, already in ro
                     inv = trav_inv<TRAV>(rd);
-                    trav_start<TRAV>(tr, stk, ETA, 5000.0f);
+                    trav_start<TRAV>(tr, stk, ETA, W8 ? w8_balls(ro, rd, ETA, 5000.0f).t : 5000.0f);
                     emit = false;
                     bounce++;
                     shadow = false;
@@ -1220,26 +1368,6 @@ __device__ __forceinline__ bool w1_triangle(f3 o, f3 w, float tmin, float& tmax,
     nrm = normalize(normal);
     return true;
 }
-__device__ __forceinline__ bool w1_sphere(f3 o, f3 w, float tmin, float& tmax, f3 center, float radius, f3& pos,
-                                          f3& nrm)
-{
-    const f3 oc = sub(o, center);
-    const float a = dot(w, w);
-    const float b2 = dot(oc, w);
-    const float c = dot(oc, oc) - radius * radius;
-    const float disc = b2 * b2 - a * c;
-    if (disc < 0.0f) return false;
-    const float ds = rt_det_sqrtf(disc);
-    float root = (-b2 - ds) / a;
-    if (root < tmin || root > tmax) {
-        root = (-b2 + ds) / a;
-        if (root < tmin || root > tmax) return false;
-    }
-    tmax = root;
-    pos = add(o, muls(w, root));
-    nrm = normalize(sub(pos, center));
-    return true;
-}
 __device__ __forceinline__ bool w1_plane(f3 o, f3 w, float tmin, float& tmax, f3 normal, f3 position, f3& pos,
                                          f3& nrm)
 {
@@ -1486,6 +1614,24 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
             else detail ? launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
                         : launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         }
+        break;
+    case RT_MODE_W8E1:
+        if (bvh) detail ? launch_path<RT_MODE_W8E1, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_path<RT_MODE_W8E1, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_path<RT_MODE_W8E1, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_path<RT_MODE_W8E1, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        break;
+    case RT_MODE_W8E2:
+        if (bvh) detail ? launch_path<RT_MODE_W8E2, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_path<RT_MODE_W8E2, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_path<RT_MODE_W8E2, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_path<RT_MODE_W8E2, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        break;
+    case RT_MODE_W8E3:
+        if (bvh) detail ? launch_path<RT_MODE_W8E3, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_path<RT_MODE_W8E3, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_path<RT_MODE_W8E3, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_path<RT_MODE_W8E3, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         break;
     case RT_MODE_W6E1:
     case RT_MODE_PROJECT: {

@@ -108,7 +108,7 @@ class RenderState:
         first = self.iteration if self.progressive else 0
         c = self.ctx.render(self.mode, self.trav, (0, 0, self.width, self.height), first, spp, self.accum.ptr,
                             self.ids.ptr, counts=counts)
-        if self.progressive and self.mode in ("W7E3", "W9E1"):
+        if self.progressive and self.mode in F.PATH_MODES:
             self.iteration += spp
         self.update()
         return c

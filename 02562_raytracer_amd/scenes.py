@@ -15,6 +15,9 @@ SHADER_MODES = {
     "project.wgsl": "PROJECT",
     "w7e3.wgsl": "W7E3",
     "w9e1.wgsl": "W9E1",
+    "w8e1.wgsl": "W8E1",
+    "w8e2.wgsl": "W8E2",
+    "w8e3.wgsl": "W8E3",
 }
 
 

@@ -90,7 +90,10 @@ typedef enum rt_mode {
     RT_MODE_W6E1    = 1,  /* res/shaders/w6e1.wgsl: primary rays, directional light, split vertex layout */
     RT_MODE_PROJECT = 2,  /* res/shaders/project.wgsl: as W6E1, combined layout, ambient*0.1 */
     RT_MODE_W7E3    = 3,  /* res/shaders/w7e3.wgsl: area-light path tracer, progressive       */
-    RT_MODE_W9E1    = 4   /* res/shaders/w9e1.wgsl: dummy-light path tracer, environment escape */
+    RT_MODE_W9E1    = 4,  /* res/shaders/w9e1.wgsl: dummy-light path tracer, environment escape */
+    RT_MODE_W8E1    = 5,  /* res/shaders/w8e1.wgsl: Cornell box + mirror and glass balls, direct light */
+    RT_MODE_W8E2    = 6,  /* res/shaders/w8e2.wgsl: as W8E1, path traced (Russian roulette, clamp 100) */
+    RT_MODE_W8E3    = 7   /* res/shaders/w8e3.wgsl: as W8E2, Beer-Lambert absorption in the glass ball */
 } rt_mode;
 
 /* SceneDescriptor.traverse_type, src/scenes.rs:13-17 */

@@ -494,6 +494,222 @@ static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
     }
 }
 
+/* ------------------------------------------------------------ W8E1 / W8E2 / W8E3
+ * Cornell box with two analytic balls (res/shaders/w8e1.wgsl, w8e2.wgsl,
+ * w8e3.wgsl).  Rays that turn NaN (sqrt of a negative cos_t^2 under total
+ * internal reflection, reflected) follow IEEE comparison semantics
+ * throughout, as the kernel does. */
+enum { SH_LAMBERTIAN = 0, SH_MIRROR = 2, SH_TRANSPARENT = 7 };
+
+static int intersect_sphere(Ray* r, Hit* h, v3 center, float radius)   /* w8e1.wgsl:352-376 */
+{
+    v3 oc = sub(r->origin, center);
+    float a = dot(r->direction, r->direction);
+    float b_over_2 = dot(oc, r->direction);
+    float c = dot(oc, oc) - radius * radius;
+    float discriminant = b_over_2 * b_over_2 - a * c;
+    if (discriminant < 0.0f) return 0;
+    float disc_sqrt = rt_det_sqrtf(discriminant);
+    float root = (-b_over_2 - disc_sqrt) / a;
+    if (root < r->tmin || root > r->tmax) {
+        root = (-b_over_2 + disc_sqrt) / a;
+        if (root < r->tmin || root > r->tmax) return 0;
+    }
+    r->tmax = root;
+    h->dist = root;
+    h->position = add(r->origin, muls(r->direction, root));   /* ray_at */
+    h->normal = normalize(sub(h->position, center));
+    return 1;
+}
+
+static int intersect_scene_w8(Ctx* C, Ray* r, Hit* h)   /* intersect_scene_bsp, w8e1.wgsl:244-262 */
+{
+    int has_hit = 0;
+    if (intersect_sphere(r, h, V(420.0f, 90.0f, 370.0f), 90.0f)) {
+        h->shader = SH_MIRROR;
+        has_hit = 1;
+    }
+    if (intersect_sphere(r, h, V(130.0f, 90.0f, 250.0f), 90.0f)) {
+        h->shader = SH_TRANSPARENT;   /* ior1_over_ior2 1.5; W8E3: extinction (0.5, 0.2, 0.2) */
+        has_hit = 1;
+    }
+    if (trace(C, r, h, 1)) {
+        h->shader = SH_LAMBERTIAN;
+        has_hit = 1;
+    }
+    return has_hit;
+}
+
+static v3 lambertian_w8(Ctx* C, Ray* r, Hit* h, uint32_t* t)
+{
+    /* w8e1.wgsl:406-435; w8e2.wgsl:444-489 adds factor, Russian roulette and
+     * setup_indirect; w8e3.wgsl scales diffuse and ambient by factor in place */
+    const or_scene* s = C->s;
+    const float ETA = 0.01f;
+    const int e3 = C->mode == OR_MODE_W8E3;
+    const or_material* m = mat_of(s, h->material);
+    v3 brdf = divs(load3(m->diffuse), PI_F);
+    v3 emission = load3(m->ambient);
+    v3 diffuse = V(0, 0, 0), ambient = V(0, 0, 0);
+    v3 normal = h->normal;
+    uint32_t light_tris = s->nlights - 1u;
+    uint32_t ri = mcg31(t);
+    uint32_t idx = (light_tris ? ri % light_tris : 0u) + 1u;
+    Light L = sample_area_light(s, h->position, idx, t);
+    Ray sr;
+    sr.direction = L.w_i;
+    sr.origin = h->position;
+    sr.tmax = L.dist - ETA;
+    sr.tmin = ETA;
+    Hit hi;
+    memset(&hi, 0, sizeof hi);
+    C->c.shadow++;
+    int blocked = intersect_scene_w8(C, &sr, &hi);
+    if (!blocked) {
+        diffuse = muls(mul(muls(brdf, rt_satf(dot(normal, L.w_i))), L.l_i), (float)light_tris);
+        if (e3) diffuse = mul(diffuse, h->factor);
+    }
+    if (h->emit) ambient = e3 ? mul(emission, h->factor) : emission;
+    if (C->mode == OR_MODE_W8E1) return add(diffuse, ambient);
+    if (!e3) diffuse = mul(diffuse, h->factor);
+    h->factor = mul(h->factor, muls(brdf, PI_F));
+    float prob = (brdf.x + brdf.y + brdf.z) / 3.0f;
+    float step = rnd(t);
+    if (step < prob) {
+        setup_indirect(r, h, t, ETA);
+        h->factor = divs(h->factor, prob);
+    }
+    return add(diffuse, ambient);
+}
+
+static v3 mirror_w8(Ctx* C, Ray* r, Hit* h)   /* w8e1.wgsl:437-445 / w8e2.wgsl:509-522 */
+{
+    const float ETA = 0.01f;
+    v3 n = h->normal, d = r->direction;
+    r->direction = sub(d, muls(n, 2.0f * dot(n, d)));   /* reflect */
+    r->origin = C->mode == OR_MODE_W8E1 ? h->position : add(h->position, muls(n, ETA));
+    r->tmax = 5000.0f;
+    r->tmin = ETA;
+    h->has_hit = 0;
+    if (C->mode != OR_MODE_W8E1) h->emit = 1;
+    return V(0, 0, 0);
+}
+
+static float fresnel_r(float cos_i, float cos_t, float ni_over_nt)   /* w8e2.wgsl:202-212 */
+{
+    float ii = ni_over_nt * cos_i, tt = 1.0f * cos_t, ti = 1.0f * cos_i, it = ni_over_nt * cos_t;
+    float r1 = (ii - tt) / (ii + tt), r2 = (ti - it) / (ti + it);
+    return 0.5f * (r1 * r1 + r2 * r2);
+}
+
+static v3 transparent_w8(Ctx* C, Ray* r, Hit* h, uint32_t* t)
+{
+    /* w8e1.wgsl:447-490, w8e2.wgsl:524-569, w8e3.wgsl (absorption on exit) */
+    const float ETA = 0.01f;
+    const int mode = C->mode;
+    v3 w_i = neg(normalize(r->direction));
+    v3 normal = normalize(h->normal);
+    v3 out_normal;
+    float ior = 1.5f;
+    float cos_i = dot(w_i, normal);
+    int entering = cos_i < 0.0f;
+    v3 T_r = V(1.0f, 1.0f, 1.0f);
+    float tprob = 0.0f;
+    if (entering) {
+        cos_i = dot(w_i, neg(normal));
+        out_normal = neg(normal);
+    } else {
+        ior = 1.0f / ior;
+        out_normal = normal;
+        if (mode == OR_MODE_W8E3) {
+            v3 dd = sub(h->position, r->origin);
+            float sd = rt_det_sqrtf(dot(dd, dd)) / 100.0f;
+            v3 nr = neg(V(0.5f, 0.2f, 0.2f));
+            T_r = V(rt_det_expf(nr.x * sd), rt_det_expf(nr.y * sd), rt_det_expf(nr.z * sd));
+            tprob = (T_r.x + T_r.y + T_r.z) / 3.0f;
+            if (tprob < 0.0f || tprob > 1.0f) return V(0.7f, 0.0f, 0.7f);   /* error_shader */
+        }
+    }
+    float cos_t2 = (1.0f - (ior * ior) * (1.0f - cos_i * cos_i));
+    float refl;
+    if (cos_t2 < 0.0f) {
+        refl = 1.0f;
+    } else {
+        refl = fresnel_r(cos_i, rt_det_sqrtf(cos_t2), ior);
+        if (mode == OR_MODE_W8E1) refl = rt_satf(refl);
+    }
+    v3 tangent = sub(muls(out_normal, cos_i), w_i);
+    v3 on = mode == OR_MODE_W8E1 ? out_normal : normalize(out_normal);
+    v3 w_t = sub(muls(tangent, ior), muls(on, rt_det_sqrtf(cos_t2)));
+    r->direction = w_t;   /* ray_init(w_t, position) */
+    r->origin = h->position;
+    r->tmax = 5000.0f;
+    r->tmin = ETA;
+    h->has_hit = 0;
+    if (mode != OR_MODE_W8E1) h->emit = 1;
+    float step = rnd(t);
+    if (step < refl) {
+        h->normal = out_normal;
+        return mirror_w8(C, r, h);
+    }
+    if (mode == OR_MODE_W8E2) {
+        h->factor = divs(h->factor, 1.0f - refl);
+    } else if (mode == OR_MODE_W8E3 && !entering) {
+        if (step < refl + tprob) h->factor = divs(mul(h->factor, T_r), refl + tprob);
+        else h->has_hit = 1;   /* absorbed */
+    }
+    return V(0, 0, 0);
+}
+
+static void sample_w8(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t it, float out[3], uint32_t* prim)
+{
+    /* fs_main, w8e1.wgsl:207-241 / w8e2.wgsl:246-281 */
+    const or_uniform* u = C->u;
+    const int e1 = C->mode == OR_MODE_W8E1;
+    const float ETA = 0.01f;
+    const v3 bg = e1 ? V(0.1f, 0.3f, 0.6f) : V(0.0f, 0.0f, 0.0f);
+    const int max_depth = e1 ? 10 : 50;
+    uint32_t t = tea16(y * u->resolution[0] + x, it);
+    float jx = rnd(&t);
+    float jy = rnd(&t);
+    jx = jx / (float)u->resolution[1];
+    jy = jy / (float)u->resolution[1];
+    float ux, uy;
+    pixel_uv(u, x, y, &ux, &uy);
+    Ray r;
+    r.direction = cam_dir(cam, ux, uy, jx, jy);
+    r.origin = cam->e;
+    r.tmax = 5000.0f;
+    r.tmin = ETA;
+    Hit h;
+    memset(&h, 0, sizeof h);
+    h.factor = V(1, 1, 1);
+    h.emit = 1;
+    v3 result = V(0, 0, 0);
+    *prim = 0xFFFFFFFFu;
+    C->c.primary++;
+    for (int i = 0; i < max_depth; i++) {
+        if (i > 0) C->c.bounce++;
+        if (intersect_scene_w8(C, &r, &h)) {
+            if (i == 0 && h.shader == SH_LAMBERTIAN) *prim = h.tri;
+            h.has_hit = 1;   /* shade() */
+            v3 c;
+            if (h.shader == SH_LAMBERTIAN) c = lambertian_w8(C, &r, &h, &t);
+            else if (h.shader == SH_MIRROR) c = mirror_w8(C, &r, &h);
+            else c = transparent_w8(C, &r, &h, &t);
+            if (!e1) c = V(rt_minf(c.x, 100.0f), rt_minf(c.y, 100.0f), rt_minf(c.z, 100.0f));   /* firefly clamp */
+            result = add(result, c);
+        } else {
+            result = add(result, bg);
+            break;
+        }
+        if (h.has_hit) break;
+    }
+    out[0] = result.x;
+    out[1] = result.y;
+    out[2] = result.z;
+}
+
 static void sample_path(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t it, float out[3],
                         uint32_t* prim)
 {
@@ -801,14 +1017,15 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
         size_t o = (size_t)ry * J->w + rx;
         float* acc = J->accum + 4 * o;
         uint32_t prim = 0xFFFFFFFFu;
-        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1) {
+        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 || J->mode >= OR_MODE_W8E1) {
             float a[3] = {acc[0], acc[1], acc[2]};
             if (J->first_iter == 0) a[0] = a[1] = a[2] = 0.0f;
             for (uint32_t k = 0; k < J->spp; k++) {
                 uint32_t it = J->first_iter + k;
                 float res[3];
                 C->c.samples++;
-                sample_path(C, cam, x, y, it, res, &prim);
+                if (J->mode >= OR_MODE_W8E1) sample_w8(C, cam, x, y, it, res, &prim);
+                else sample_path(C, cam, x, y, it, res, &prim);
                 /* fs_main accumulation, w7e3.wgsl:261-271 */
                 for (int c = 0; c < 3; c++) {
                     float curr_sum = a[c] * (float)it;
@@ -856,13 +1073,13 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
               uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
               float* accum, uint32_t* ids, or_counts* counts, int nthreads)
 {
-    if (mode < 0 || mode > 4) return -1;
+    if (mode < 0 || mode > OR_MODE_W8E3) return -1;
     if (mode != OR_MODE_W1E6) {
         if (!s || !s->nmats) return -1;
         if (trav == OR_TRAV_BSP && (!s->tree || !s->planes)) return -1;
         if (trav == OR_TRAV_BVH && !s->bvh_nodes) return -1;
         if (trav == OR_TRAV_NONE) return -1;
-        if (mode == OR_MODE_W7E3 && s->nlights < 2) return -1;
+        if ((mode == OR_MODE_W7E3 || mode >= OR_MODE_W8E1) && s->nlights < 2) return -1;
     }
     if (x0 + w > u->resolution[0] || y0 + h > u->resolution[1]) return -1;
     Job J;
