@@ -753,43 +753,6 @@ __device__ __forceinline__ W8Ball w8_balls(f3 o, f3 w, float tmin, float tmax)
     return b;
 }
 
-// intersect_plane (w9e2.wgsl:388-404): the holdout plane through the origin
-// with normal (0, 1, 0), in the shader's arithmetic
-__device__ __forceinline__ bool w9_plane(f3 o, f3 w, float tmin, float& tmax)
-{
-    const f3 n = V(0.0f, 1.0f, 0.0f);
-    const float distance = dot(sub(V(0.0f, 0.0f, 0.0f), o), n) / dot(w, n);
-    if (distance < tmin || distance > tmax) return false;
-    tmax = distance;
-    return true;
-}
-
-// tmax of a closest-hit ray [ETA, 5000] from o along w: the analytic objects
-// the shader tests before intersect_trimesh bound the mesh walk (r.tmax)
-template <int MODE>
-__device__ __forceinline__ float ray_tmax(f3 o, f3 w, float eta)
-{
-    float tm = 5000.0f;
-    if (MODE == RT_MODE_W8E1 || MODE == RT_MODE_W8E2 || MODE == RT_MODE_W8E3) tm = w8_balls(o, w, eta, 5000.0f).t;
-    if (MODE == RT_MODE_W9E2) w9_plane(o, w, eta, tm);
-    return tm;
-}
-
-// environment_map(dir) of the W9 modes (w9e1.wgsl:232-239; w9e2.wgsl:234-246
-// decodes RGBE): the texture if one is set, else the constant environment
-template <int MODE>
-__device__ __forceinline__ f3 env_at(const DevLaunch& L, const f3 env, const f3 d)
-{
-    f3 e = env;
-    if (RT_ENV_TEX && L.env_tex) {
-        float rgb[3];
-        if (MODE == RT_MODE_W9E2) rt_det_env_sample_rgbe(L.env_tex, L.env_w, L.env_h, d.x, d.y, d.z, rgb);
-        else rt_det_env_sample(L.env_tex, L.env_w, L.env_h, d.x, d.y, d.z, rgb);
-        e = V(rgb[0], rgb[1], rgb[2]);
-    }
-    return e;
-}
-
 // Shading of a ball hit (shade(), w8e1.wgsl:379-404): mirror (id 1,
 // w8e1.wgsl:437-445 / w8e2.wgsl:509-522) or transparent (id 2,
 // w8e1.wgsl:447-490 / w8e2.wgsl:524-569 / w8e3.wgsl: absorption on exit).
@@ -883,11 +846,8 @@ k_path(DevScene S, DevLaunch L)
                                         : lds_stack + threadIdx.x;
     const BvhDeep dp{TRAV == RT_TRAVERSE_BVH ? L.bvh_deep + (size_t)blockIdx.x * 256u + threadIdx.x : nullptr,
                      gridDim.x * 256u};
-    // W9E2: W9E1 + the holdout plane y = 0 (ambient-occlusion ray, environment
-    // seen through it) and an RGBE environment; one instantiation for all its shaders
-    constexpr bool W9E2 = MODE == RT_MODE_W9E2;
-    constexpr bool W9 = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT || W9E2;
-    constexpr bool XT = MODE == MODE_W9E1_TRANSPARENT || W9E2;
+    constexpr bool W9 = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT;
+    constexpr bool XT = MODE == MODE_W9E1_TRANSPARENT;
     // W8E1/W8E2/W8E3: the Cornell box with its two analytic balls; W8E1 lights
     // directly only (10 segments), W8E2/W8E3 path trace with a firefly clamp
     constexpr bool W8 = MODE == RT_MODE_W8E1 || MODE == RT_MODE_W8E2 || MODE == RT_MODE_W8E3;
@@ -916,13 +876,12 @@ k_path(DevScene S, DevLaunch L)
     // lane state: ST_IDLE (no pixel), ST_TRACE (a ray in flight), ST_SHADE (ray done, waiting to shade)
     enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2 };
     uint32_t st = ST_IDLE;
-    bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false, ao = false;
+    bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false;
     uint32_t px = 0, py = 0, out = 0, it = 0, unit_end = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
     f3 res = V(0, 0, 0), fac = V(1, 1, 1), ro = V(0, 0, 0), rd = V(0, 0, 1), inv = V(0, 0, 0);
     f3 ndir = V(0, 0, 1), cu = V(0, 0, 0), cb = V(0, 0, 0);
     Trav tr;
     trav_init(tr, 0.0f, 0.0f);
-
 
     // fs_main prologue for iteration `it` of the lane's pixel (w7e3.wgsl:236-248)
     auto start_sample = [&]() {
@@ -942,9 +901,8 @@ k_path(DevScene S, DevLaunch L)
         prim = 0xFFFFFFFFu;
         shadow = false;
         inv = trav_inv<TRAV>(rd);
-        trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
+        trav_start<TRAV>(tr, stk, ETA, W8 ? w8_balls(ro, rd, ETA, 5000.0f).t : 5000.0f);
         st = ST_TRACE;
-        ao = false;
         cnt.v[C_SAMPLES]++;
         cnt.v[C_PRIMARY]++;
     };
@@ -1040,10 +998,8 @@ k_path(DevScene S, DevLaunch L)
                         shadow = true;
                         st = ST_TRACE;
                         cnt.v[C_SHADOW]++;
-                        float tpl = Lt.dist - ETA;
-                        if ((W8 && w8_balls(ro, rd, ETA, Lt.dist - ETA).id != 0u) ||
-                            (W9E2 && w9_plane(ro, rd, ETA, tpl))) {
-                            tr.found = true;   // a ball / the plane blocks the light: no mesh walk
+                        if (W8 && w8_balls(ro, rd, ETA, Lt.dist - ETA).id != 0u) {
+                            tr.found = true;   // a ball blocks the light: no mesh walk
                             st = ST_SHADE;
                         } else {
                             trav_start<TRAV>(tr, stk, ETA, Lt.dist - ETA);
@@ -1099,7 +1055,7 @@ k_path(DevScene S, DevLaunch L)
                         if (bounce + 1u < 50u) {
                             bounce++;
                             inv = trav_inv<TRAV>(rd);
-                            trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
+                            trav_start<TRAV>(tr, stk, ETA, 5000.0f);
                             st = ST_TRACE;
                             cnt.v[C_BOUNCE]++;
                         } else {
@@ -1121,44 +1077,31 @@ k_path(DevScene S, DevLaunch L)
                         if (w8_ball_shade<MODE>(ball, ro, rd, fac, emit, res, rng, ETA) && bounce + 1u < MAXD) {
                             bounce++;
                             inv = trav_inv<TRAV>(rd);
-                            trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
+                            trav_start<TRAV>(tr, stk, ETA, w8_balls(ro, rd, ETA, 5000.0f).t);
                             st = ST_TRACE;
                             cnt.v[C_BOUNCE]++;
                         } else {
                             sample_done = true;
                         }
                     } else {
-                        float tpl = 5000.0f;
-                        if (W9E2 && w9_plane(ro, rd, ETA, tpl)) {
-                            // holdout_shader (w9e2.wgsl:514-537): an any-hit ambient-occlusion
-                            // ray about the plane normal; unoccluded, the environment behind
-                            ndir = rd;
-                            ro = add(ro, muls(rd, tpl));   // ray_at
-                            rd = indirect_dir(V(0.0f, 1.0f, 0.0f), rng);
-                            inv = trav_inv<TRAV>(rd);
-                            trav_start<TRAV>(tr, stk, ETA, 5000.0f);
-                            shadow = true;
-                            ao = true;
-                            st = ST_TRACE;
-                            cnt.v[C_SHADOW]++;
-                        } else {
-                            // miss: background (w7e3, w8e*) / environment_map(dir) * factor (w9e1.wgsl:264-265)
-                            res = add(res, W9 ? mul(env_at<MODE>(L, env, rd), fac) : (W8E1 ? V(0.1f, 0.3f, 0.6f) : V(0, 0, 0)));
-                            sample_done = true;
+                        // miss: background (w7e3, w8e*) / environment_map(dir) * factor (w9e1.wgsl:264-265)
+                        f3 e = env;
+                        if (RT_ENV_TEX && W9 && L.env_tex) {
+                            float rgb[3];
+                            rt_det_env_sample(L.env_tex, L.env_w, L.env_h, rd.x, rd.y, rd.z, rgb);
+                            e = V(rgb[0], rgb[1], rgb[2]);
                         }
+                        res = add(res, W9 ? mul(e, fac) : (W8E1 ? V(0.1f, 0.3f, 0.6f) : V(0, 0, 0)));
+                        sample_done = true;
                     }
                 }
-            } else if (W9E2 && ao) {
-                // ambient-occlusion ray finished: occluded adds vec3(0); the sample ends
-                res = add(res, tr.found ? V(0, 0, 0) : mul(env_at<MODE>(L, env, ndir), fac));
-                sample_done = true;
             } else {
                 // shadow ray finished: rest of lambertian, then the bounce
                 res = add(res, tr.found ? cb : cu);
                 if (survive && bounce + 1u < MAXD) {
                     rd = ndir;   // origin = hit position, already in ro
                     inv = trav_inv<TRAV>(rd);
-                    trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
+                    trav_start<TRAV>(tr, stk, ETA, W8 ? w8_balls(ro, rd, ETA, 5000.0f).t : 5000.0f);
                     emit = false;
                     bounce++;
                     shadow = false;
@@ -1575,8 +1518,6 @@ __host__ __device__ inline void math_eval(float x, float* o)
     o[9] = xx / dd;
     o[10] = rt_det_atan2f(x, 1.3f - x * 0.9f);   // environment_map's atan2 (w9e1.wgsl:236)
     o[11] = rt_det_atanf(x * 5.0f);
-    o[12] = rt_det_expf(x * 30.0f);    // over- and underflow at |x| > 2.96 / 3.47
-    o[13] = rt_det_exp2f(x * 40.0f);   // the RGBE decode's pow(2, e) (w9e2.wgsl:244); subnormal below -126
 }
 __global__ void k_selftest_math(const float* in, float* out, uint32_t n)
 {
@@ -1673,12 +1614,6 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
             else detail ? launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
                         : launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         }
-        break;
-    case RT_MODE_W9E2:
-        if (bvh) detail ? launch_path<RT_MODE_W9E2, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
-                        : launch_path<RT_MODE_W9E2, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
-        else detail ? launch_path<RT_MODE_W9E2, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
-                    : launch_path<RT_MODE_W9E2, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         break;
     case RT_MODE_W8E1:
         if (bvh) detail ? launch_path<RT_MODE_W8E1, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)

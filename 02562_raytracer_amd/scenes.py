@@ -18,6 +18,7 @@ SHADER_MODES = {
     "w8e1.wgsl": "W8E1",
     "w8e2.wgsl": "W8E2",
     "w8e3.wgsl": "W8E3",
+    "w9e2.wgsl": "W9E2",
 }
 
 

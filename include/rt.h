@@ -93,7 +93,8 @@ typedef enum rt_mode {
     RT_MODE_W9E1    = 4,  /* res/shaders/w9e1.wgsl: dummy-light path tracer, environment escape */
     RT_MODE_W8E1    = 5,  /* res/shaders/w8e1.wgsl: Cornell box + mirror and glass balls, direct light */
     RT_MODE_W8E2    = 6,  /* res/shaders/w8e2.wgsl: as W8E1, path traced (Russian roulette, clamp 100) */
-    RT_MODE_W8E3    = 7   /* res/shaders/w8e3.wgsl: as W8E2, Beer-Lambert absorption in the glass ball */
+    RT_MODE_W8E3    = 7,  /* res/shaders/w8e3.wgsl: as W8E2, Beer-Lambert absorption in the glass ball */
+    RT_MODE_W9E2    = 8   /* res/shaders/w9e2.wgsl: W9E1 + holdout plane y=0 (AO any-hit), RGBE environment */
 } rt_mode;
 
 /* SceneDescriptor.traverse_type, src/scenes.rs:13-17 */

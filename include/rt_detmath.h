@@ -160,6 +160,25 @@ RT_HD float rt_det_expf(float x)
     return __builtin_ldexpf(__builtin_ldexpf(y, n1), n2);
 }
 
+/* exp2: Cephes exp2f (round-to-nearest integer split, degree-6 polynomial on
+ * [-0.5, 0.5]), scaled by ldexp (exact).  Exact powers of two for integer x.
+ * Used as WGSL pow(2.0, e) by W9E2's RGBE environment decode
+ * (w9e2.wgsl:240-245). */
+RT_HD float rt_det_exp2f(float x)
+{
+    if (x != x) return x;
+    if (x > 128.0f) return __builtin_inff();
+    if (x < -151.0f) return 0.0f;
+    const float i0 = __builtin_floorf(x + 0.5f);
+    const float f = x - i0;
+    float px = f * (((((1.535336188319500e-4f * f + 1.339887440266574e-3f) * f + 9.618437357674640e-3f) * f
+                      + 5.550332471162809e-2f) * f + 2.402264791363012e-1f) * f + 6.931472028550421e-1f);
+    px = 1.0f + px;
+    const int n = (int)i0;
+    const int n1 = n / 2, n2 = n - n1;
+    return __builtin_ldexpf(__builtin_ldexpf(px, n1), n2);
+}
+
 /* atan on |x| <= tan(pi/8) after the Cephes atanf reduction */
 RT_HD float rt_det_atanf(float x)
 {
@@ -231,6 +250,40 @@ RT_HD void rt_det_env_sample(const unsigned int* tex, unsigned int w, unsigned i
         rgb[c] = rt_det__unorm8((t00 >> sh) & 255u) * w00 + rt_det__unorm8((t10 >> sh) & 255u) * w10 +
                  rt_det__unorm8((t01 >> sh) & 255u) * w01 + rt_det__unorm8((t11 >> sh) & 255u) * w11;
     }
+}
+
+/* environment_map of w9e2.wgsl:234-246: the same lookup on an RGBE-encoded
+ * texture (luxo_pxr_campus.hdr.png): all four channels filtered, then
+ * rgb * pow(2, a*255 - 128) on the filtered alpha, as the shader decodes after
+ * textureSample. */
+RT_HD void rt_det_env_sample_rgbe(const unsigned int* tex, unsigned int w, unsigned int h, float dx, float dy,
+                                  float dz, float* rgb)
+{
+    const float u = 0.5f * (1.0f + (1.0f / RT_DET_PIF) * rt_det_atan2f(dx, -dz));
+    const float v = 1.0f / RT_DET_PIF * rt_det_acosf(-dy);
+    const float s = u, t = 1.0f - v;
+    float x = s * (float)w - 0.5f, y = t * (float)h - 0.5f;
+    x = x == x ? x : 0.0f;
+    y = y == y ? y : 0.0f;
+    const float fx = __builtin_floorf(x), fy = __builtin_floorf(y);
+    const float a = x - fx, b = y - fy;
+    int x0 = (int)fx, y0 = (int)fy, x1 = x0 + 1, y1 = y0 + 1;
+    const int wm = (int)w - 1, hm = (int)h - 1;
+    x0 = x0 < 0 ? 0 : (x0 > wm ? wm : x0);
+    x1 = x1 < 0 ? 0 : (x1 > wm ? wm : x1);
+    y0 = y0 < 0 ? 0 : (y0 > hm ? hm : y0);
+    y1 = y1 < 0 ? 0 : (y1 > hm ? hm : y1);
+    const unsigned int t00 = tex[(unsigned int)y0 * w + (unsigned int)x0], t10 = tex[(unsigned int)y0 * w + (unsigned int)x1];
+    const unsigned int t01 = tex[(unsigned int)y1 * w + (unsigned int)x0], t11 = tex[(unsigned int)y1 * w + (unsigned int)x1];
+    const float w00 = (1.0f - a) * (1.0f - b), w10 = a * (1.0f - b), w01 = (1.0f - a) * b, w11 = a * b;
+    float c4[4];
+    for (int c = 0; c < 4; c++) {
+        const unsigned int sh = 8u * (unsigned int)c;
+        c4[c] = rt_det__unorm8((t00 >> sh) & 255u) * w00 + rt_det__unorm8((t10 >> sh) & 255u) * w10 +
+                rt_det__unorm8((t01 >> sh) & 255u) * w01 + rt_det__unorm8((t11 >> sh) & 255u) * w11;
+    }
+    const float e = rt_det_exp2f(c4[3] * 255.0f - 128.0f);
+    for (int c = 0; c < 3; c++) rgb[c] = c4[c] * e;
 }
 
 #endif /* RT02562_DETMATH_H */

@@ -383,12 +383,83 @@ static v3 shade_w7e3(Ctx* C, Ray* r, Hit* h, uint32_t* t)
     return add(diffuse, ambient);
 }
 
+/* ------------------------------------------------------------ W9E2 additions
+ * res/shaders/w9e2.wgsl: the holdout plane y = 0 tested before the mesh, its
+ * ambient-occlusion shader, and the RGBE environment decode. */
+#define SH_HOLDOUT 8u
+
+static v3 env_lookup(Ctx* C, v3 d)   /* environment_map, w9e1.wgsl:232-239 / w9e2.wgsl:234-246 */
+{
+    v3 e = load3(C->s->env);
+    if (C->s->env_tex) {
+        float rgb[3];
+        if (C->mode == OR_MODE_W9E2)
+            rt_det_env_sample_rgbe(C->s->env_tex, C->s->env_w, C->s->env_h, d.x, d.y, d.z, rgb);
+        else
+            rt_det_env_sample(C->s->env_tex, C->s->env_w, C->s->env_h, d.x, d.y, d.z, rgb);
+        e = V(rgb[0], rgb[1], rgb[2]);
+    }
+    return e;
+}
+
+static int intersect_plane_w9e2(Ray* r, Hit* h)   /* intersect_plane, w9e2.wgsl:388-404 */
+{
+    v3 normal = V(0.0f, 1.0f, 0.0f), position = V(0.0f, 0.0f, 0.0f);
+    float distance = dot(sub(position, r->origin), normal) / dot(r->direction, normal);
+    if (distance < r->tmin || distance > r->tmax) return 0;
+    r->tmax = distance;
+    h->dist = distance;
+    h->position = add(r->origin, muls(r->direction, distance));
+    h->normal = normal;
+    return 1;
+}
+
+static int intersect_scene_w9e2(Ctx* C, Ray* r, Hit* h)   /* intersect_scene_bsp, w9e2.wgsl:290-304 */
+{
+    int has_hit = 0;
+    if (intersect_plane_w9e2(r, h)) {
+        h->shader = SH_HOLDOUT;
+        has_hit = 1;
+    }
+    if (trace(C, r, h, 0)) {
+        h->shader = C->u->selection1;
+        has_hit = 1;
+    }
+    return has_hit;
+}
+
+static v3 holdout_w9e2(Ctx* C, Ray* r, Hit* h, uint32_t* t)   /* holdout_shader, w9e2.wgsl:514-537 */
+{
+    const float ETA = 0.0001f;
+    Ray ao;
+    Hit hi;
+    memset(&hi, 0, sizeof hi);
+    v3 normal = normalize(h->normal);
+    float xi1 = rnd(t);
+    float xi2 = rnd(t);
+    float thet = rt_det_acosf(rt_det_sqrtf(1.0f - xi1));
+    float phi = 2.0f * PI_F * xi2;
+    float st = rt_det_sinf(thet), ct = rt_det_cosf(thet);
+    v3 tang = V(st * rt_det_cosf(phi), st * rt_det_sinf(phi), ct);
+    ao.direction = rotate_to_normal(normal, tang);
+    ao.origin = h->position;
+    ao.tmin = ETA;
+    ao.tmax = 5000.0f;
+    C->c.shadow++;
+    /* intersect_trimesh_immediate_return (bsp.wgsl:83-155): the same walk as
+     * intersect_trimesh up to its first accepted triangle, so the same boolean */
+    if (trace(C, &ao, &hi, 0)) return V(0, 0, 0);
+    h->has_hit = 1;
+    return mul(env_lookup(C, r->direction), h->factor);
+}
+
 static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
 {
     /* shade (w9e1.wgsl) with selection1; lambertian with light_init() (:428-470) */
     const or_scene* s = C->s;
     const float ETA = 0.0001f;
     h->has_hit = 1;
+    if (C->mode == OR_MODE_W9E2 && h->shader == SH_HOLDOUT) return holdout_w9e2(C, r, h, t);
     const or_material* m = mat_of(s, h->material);
     switch (C->u->selection1) {
     case 0: {
@@ -408,7 +479,7 @@ static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
         Hit hi;
         memset(&hi, 0, sizeof hi);
         C->c.shadow++;
-        int blocked = trace(C, &sr, &hi, 0);
+        int blocked = C->mode == OR_MODE_W9E2 ? intersect_scene_w9e2(C, &sr, &hi) : trace(C, &sr, &hi, 0);
         if (!blocked) diffuse = mul(muls(brdf, rt_satf(dot(normal, L.w_i))), L.l_i);
         if (h->emit) ambient = mul(emission, h->factor);
         diffuse = mul(diffuse, h->factor);
@@ -714,7 +785,7 @@ static void sample_path(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t
                         uint32_t* prim)
 {
     const or_uniform* u = C->u;
-    int w9 = C->mode == OR_MODE_W9E1;
+    int w9 = C->mode == OR_MODE_W9E1 || C->mode == OR_MODE_W9E2;
     float eta = w9 ? 0.0001f : 0.01f;
     uint32_t launch_idx = y * u->resolution[0] + x;
     uint32_t t = tea16(launch_idx, it);
@@ -738,21 +809,13 @@ static void sample_path(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t
     C->c.primary++;
     for (int i = 0; i < 50; i++) {
         if (i > 0) C->c.bounce++;
-        int hit = trace(C, &r, &h, !w9);
+        int hit = C->mode == OR_MODE_W9E2 ? intersect_scene_w9e2(C, &r, &h) : trace(C, &r, &h, !w9);
         if (hit) {
-            if (i == 0) *prim = h.tri;
+            if (i == 0 && !(C->mode == OR_MODE_W9E2 && h.shader == SH_HOLDOUT)) *prim = h.tri;
             result = add(result, w9 ? shade_w9e1(C, &r, &h, &t) : shade_w7e3(C, &r, &h, &t));
         } else {
-            if (w9) {   /* environment_map(r.direction) * hit.factor, w9e1.wgsl:264-265 */
-                v3 e = load3(C->s->env);
-                if (C->s->env_tex) {
-                    float rgb[3];
-                    rt_det_env_sample(C->s->env_tex, C->s->env_w, C->s->env_h, r.direction.x, r.direction.y,
-                                      r.direction.z, rgb);
-                    e = V(rgb[0], rgb[1], rgb[2]);
-                }
-                result = add(result, mul(e, h.factor));
-            }
+            if (w9)   /* environment_map(r.direction) * hit.factor, w9e1.wgsl:264-265 */
+                result = add(result, mul(env_lookup(C, r.direction), h.factor));
             /* W7E3: + BACKGROUND_COLOR (0,0,0) */
             else result = add(result, V(0, 0, 0));
             break;
@@ -1017,14 +1080,14 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
         size_t o = (size_t)ry * J->w + rx;
         float* acc = J->accum + 4 * o;
         uint32_t prim = 0xFFFFFFFFu;
-        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 || J->mode >= OR_MODE_W8E1) {
+        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 || J->mode >= OR_MODE_W8E1) {   /* progressive */
             float a[3] = {acc[0], acc[1], acc[2]};
             if (J->first_iter == 0) a[0] = a[1] = a[2] = 0.0f;
             for (uint32_t k = 0; k < J->spp; k++) {
                 uint32_t it = J->first_iter + k;
                 float res[3];
                 C->c.samples++;
-                if (J->mode >= OR_MODE_W8E1) sample_w8(C, cam, x, y, it, res, &prim);
+                if (J->mode >= OR_MODE_W8E1 && J->mode <= OR_MODE_W8E3) sample_w8(C, cam, x, y, it, res, &prim);
                 else sample_path(C, cam, x, y, it, res, &prim);
                 /* fs_main accumulation, w7e3.wgsl:261-271 */
                 for (int c = 0; c < 3; c++) {
@@ -1073,13 +1136,13 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
               uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
               float* accum, uint32_t* ids, or_counts* counts, int nthreads)
 {
-    if (mode < 0 || mode > OR_MODE_W8E3) return -1;
+    if (mode < 0 || mode > OR_MODE_W9E2) return -1;
     if (mode != OR_MODE_W1E6) {
         if (!s || !s->nmats) return -1;
         if (trav == OR_TRAV_BSP && (!s->tree || !s->planes)) return -1;
         if (trav == OR_TRAV_BVH && !s->bvh_nodes) return -1;
         if (trav == OR_TRAV_NONE) return -1;
-        if ((mode == OR_MODE_W7E3 || mode >= OR_MODE_W8E1) && s->nlights < 2) return -1;
+        if ((mode == OR_MODE_W7E3 || (mode >= OR_MODE_W8E1 && mode <= OR_MODE_W8E3)) && s->nlights < 2) return -1;
     }
     if (x0 + w > u->resolution[0] || y0 + h > u->resolution[1]) return -1;
     Job J;
