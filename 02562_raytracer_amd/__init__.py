@@ -12,9 +12,10 @@ from . import _ffi
 from ._ffi import MODES, TRAVERSALS, RtError, lib
 from .core import BspTree, Bvh, Context, DeviceBuffer, Mesh, load_texture_rgba8, local_tiles, make_uniform
 from .render_state import ASSETS, RenderState
+from .camera import CameraController
 from .scenes import Camera, SceneDescriptor, find_scene, get_scenes
 
-__all__ = ["BspTree", "Bvh", "Camera", "Context", "DeviceBuffer", "Mesh", "RenderState", "RtError",
+__all__ = ["BspTree", "Bvh", "Camera", "CameraController", "Context", "DeviceBuffer", "Mesh", "RenderState", "RtError",
            "SceneDescriptor", "ASSETS", "MODES", "TRAVERSALS", "find_scene", "get_scenes", "lib", "local_tiles",
            "load_texture_rgba8",
            "make_uniform", "_ffi"]

@@ -18,6 +18,7 @@ import os
 import numpy as np
 
 from . import _ffi as F
+from .camera import Camera, CameraController
 from .core import BspTree, Bvh, Context, Mesh, make_uniform
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -36,6 +37,8 @@ class RenderState:
         self.device_build = device_build   # build the BSP / HLBVH on the GPU (same arrays)
         self.progressive = True
         self.iteration = 0
+        self.max_iterations = 2   # Uniform::max_iterations, SetSamples (lib.rs:472-479)
+        self.camera_controller = CameraController()
         self.setup_rendering(scene)
 
     def _background(self, scene):
@@ -53,6 +56,7 @@ class RenderState:
         if scene.mode is None:
             raise F.RtError(F.RT_E_UNSUPPORTED, f"{scene.shader} is outside the hot path (SURVEY.md section 2)")
         self.scene = scene
+        self.camera = Camera.from_tuple(scene.camera)
         self.mode = scene.mode
         self.width, self.height = self.resolution or scene.res
         self.mesh = self.bsp = self.bvh = None
@@ -93,19 +97,48 @@ class RenderState:
         return Mesh.from_obj(path)
 
     def load_scene(self, scene):
-        """RenderState::load_scene (render_state.rs:314-334): full rebuild."""
+        """RenderState::load_scene (render_state.rs:314-334): full rebuild;
+        the iteration restarts (Command::LoadScene, lib.rs:464-469)."""
+        self.iteration = 0
         self.setup_rendering(scene)
 
-    # render_state.rs:467-481
+    # render_state.rs:467-481: the controller moves the camera, then the uniform follows
     def update(self):
-        cam = self.scene.camera
-        self.uniform = make_uniform(cam.eye, cam.target, cam.up, cam.constant, self.width, self.height,
+        self.camera.aspect = float(np.float32(self.width) / np.float32(self.height))
+        self.camera_controller.update_camera(self.camera)
+        eye, target, up, constant = self.camera.as_args()
+        self.uniform = make_uniform(eye, target, up, constant, self.width, self.height,
                                     selection1=self.selection1, iteration=self.iteration)
         self.ctx.set_uniforms(self.uniform)
 
+    def input(self, key, pressed=True):
+        """RenderState::input_alt (render_state.rs:462-465): a key event for the
+        camera controller; takes effect at the next update()."""
+        return self.camera_controller.handle_camera_commands(key, pressed)
+
+    def set_camera_constant(self, constant):
+        """Command::SetCameraConstant (lib.rs:401-403)."""
+        self.camera.constant = float(constant)
+
+    def set_samples(self, samples, enabled):
+        """Command::SetSamples (lib.rs:472-479): progressive rendering up to
+        `samples` iterations, or (disabled) a frame per step at a fixed iteration."""
+        self.progressive = bool(enabled)
+        self.max_iterations = int(samples) if enabled else 2
+
+    def step(self):
+        """One pass of rendering_thread (lib.rs:331-363): render while
+        progressive and below max_iterations (or always when not progressive),
+        advance the iteration when progressive, then update().  Returns whether
+        a frame was rendered."""
+        if self.progressive and self.iteration >= self.max_iterations:
+            return False
+        self.render(1)
+        return True
+
     # render_state.rs:483-561 (+ lib.rs:349-354 iteration advance)
     def render(self, spp=1, counts=False):
-        first = self.iteration if self.progressive else 0
+        first = self.iteration   # not progressive: the iteration stays (lib.rs:350-355)
         c = self.ctx.render(self.mode, self.trav, (0, 0, self.width, self.height), first, spp, self.accum.ptr,
                             self.ids.ptr, counts=counts)
         if self.progressive and self.mode in F.PATH_MODES:
