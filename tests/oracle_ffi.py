@@ -267,7 +267,7 @@ def render(scene, uniform, mode, trav, region, first_iter=0, spp=1, accum=None, 
         jitter = np.ascontiguousarray(jitter, dtype=np.float32)
         jp = jitter.ctypes.data_as(f32p)
     if nthreads is None:
-        nthreads = os.cpu_count() or 1
+        nthreads = min(16, os.cpu_count() or 1)   # the GPU box shares 16 host threads per GPU
     rc = L.or_render(C.byref(scene.s), C.byref(uniform), jp, MODES[mode] if isinstance(mode, str) else mode,
                      TRAVS[trav] if isinstance(trav, str) else trav, x0, y0, w, h, first_iter, spp,
                      accum.ctypes.data_as(f32p), ids.ctypes.data_as(u32p), C.byref(cnt), nthreads)
