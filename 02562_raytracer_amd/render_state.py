@@ -19,6 +19,7 @@ import numpy as np
 
 from . import _ffi as F
 from .camera import Camera, CameraController
+from .jitter import MAX_SUBDIVISION, jitters_for
 from .core import BspTree, Bvh, Context, Mesh, make_uniform
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -38,6 +39,7 @@ class RenderState:
         self.progressive = True
         self.iteration = 0
         self.max_iterations = 2   # Uniform::max_iterations, SetSamples (lib.rs:472-479)
+        self.subdivision_level = 1   # Uniform.subdivision_level (uniform.rs:122-129)
         self.camera_controller = CameraController()
         self.setup_rendering(scene)
 
@@ -108,8 +110,15 @@ class RenderState:
         self.camera_controller.update_camera(self.camera)
         eye, target, up, constant = self.camera.as_args()
         self.uniform = make_uniform(eye, target, up, constant, self.width, self.height,
-                                    selection1=self.selection1, iteration=self.iteration)
-        self.ctx.set_uniforms(self.uniform)
+                                    selection1=self.selection1, iteration=self.iteration,
+                                    subdiv=self.subdivision_level)
+        # UniformGpu::update_buffer (uniform.rs:163-175): the jitter table with the uniforms
+        self.ctx.set_uniforms(self.uniform, jitters_for(self.height, self.subdivision_level))
+
+    def set_subdivision_level(self, level):
+        """Uniform::update_subdivision_level (uniform.rs:122-129): clamped to 10;
+        W6E1/PROJECT take level^2 stratified samples per pixel."""
+        self.subdivision_level = min(int(level), MAX_SUBDIVISION)
 
     def input(self, key, pressed=True):
         """RenderState::input_alt (render_state.rs:462-465): a key event for the
