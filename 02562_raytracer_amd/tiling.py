@@ -52,5 +52,12 @@ def gather_tiles(dist, acc_local, ids_local, acc_all, ids_all):
         dist.all_gather_into_tensor(ids_all, ids_local)
         return
     world = dist.get_world_size()
+    if acc_local.is_cuda:   # gloo rehearsal of the device path: through host memory
+        ha, hi = acc_all.cpu(), ids_all.cpu()
+        dist.all_gather(list(ha.chunk(world)), acc_local.cpu())
+        dist.all_gather(list(hi.chunk(world)), ids_local.cpu())
+        acc_all.copy_(ha)
+        ids_all.copy_(hi)
+        return
     dist.all_gather(list(acc_all.chunk(world)), acc_local)
     dist.all_gather(list(ids_all.chunk(world)), ids_local)

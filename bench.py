@@ -82,6 +82,16 @@ def cpu_baseline(wl, trav, mesh, accel, spp, W, H, budget_s):
                       f"{W}x{H} frame, first {it} of its {spp} spp, {el:.1f} s"}
 
 
+def all_reduce(dist, t, op):
+    """In place on the device under RCCL; through host memory under gloo."""
+    if dist.get_backend() == "nccl":
+        dist.all_reduce(t, op=op)
+        return t
+    h = t.cpu()
+    dist.all_reduce(h, op=op)
+    return h.to(t.device)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,9 +118,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knob: RT_BENCH_DEVICE pins every rank to one device (N ranks
+    # sharing a single GPU exercise the N>1 path where only one GPU exists)
+    if os.environ.get("RT_BENCH_DEVICE") is not None:
+        local = int(os.environ["RT_BENCH_DEVICE"])
+    # RCCL (backend "nccl"); RT_BENCH_DIST_BACKEND=gloo is the rehearsal path
+    # with RT_BENCH_DEVICE (RCCL refuses two ranks on one GPU): host gathers
+    backend = os.environ.get("RT_BENCH_DIST_BACKEND", "nccl")
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -190,7 +210,7 @@ def main():
                          counts["bounce"], algorithmic_bytes(detail, trav)],
                         dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(rays)
+        rays = all_reduce(dist, rays, dist.ReduceOp.SUM)
     rays = rays.cpu().numpy()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
@@ -215,7 +235,7 @@ def main():
     render_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     t = torch.tensor([elapsed, kern_ms, render_ms], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t = all_reduce(dist, t, dist.ReduceOp.MAX)
     elapsed, kern_ms, render_ms = [float(x) for x in t.cpu().numpy()]
 
     value = rays[0] * args.steps / elapsed / 1e6
