@@ -1406,6 +1406,156 @@ __global__ void __launch_bounds__(256) k_primary(DevScene S, DevLaunch L, int pr
     flush_counters(cnt, L.counters, COUNT);
 }
 
+// ------------------------------------------------------------------ W6E2 / W7E1 / W7E2 kernel
+// The Cornell-box direct-lighting worksheet shaders (w6e2.wgsl, w7e1.wgsl,
+// w7e2.wgsl): the shader is always LAMBERTIAN, so a sample is one closest-hit
+// ray plus one any-hit shadow ray per area-light triangle, and ends.  One
+// lane per pixel (a trip-free walk per ray, as k_primary): these scenes have
+// 36 triangles.  W6E2 averages subdiv^2 jittered samples (no progression);
+// W7E1/W7E2 run iterations first_iter.. in order and fold each into the
+// accumulation as fs_main does, without the max(., 0) of W7E3.
+template <int MODE>
+__device__ __forceinline__ Light direct_light(const DevScene& S, f3 pos, uint32_t idx, uint32_t& rng)
+{
+    // sample_area_light: w6e2.wgsl:245-262, w7e1.wgsl:327-346 (centre, no 1/d^2),
+    // w7e2.wgsl:327-354 (random point, 1/d^2); cos_l unclamped in all three
+    const uint32_t li = S.lights[idx < S.nlights ? idx : S.nlights - 1u];
+    const uint4 tri = S.tri_idx[li < S.ntris ? li : S.ntris - 1u];
+    const f3 v0 = ld3(S.pos[tri.x]), v1 = ld3(S.pos[tri.y]), v2 = ld3(S.pos[tri.z]);
+    const f3 cr = cross(sub(v0, v1), sub(v0, v2));
+    const float area = 0.5f * rt_det_sqrtf(dot(cr, cr));
+    const f3 l_e = ld3(mat_of(S, tri.w).ambient);
+    f3 point;
+    if (MODE == RT_MODE_W7E2) {
+        const float psi1 = rt_det_sqrtf(rnd(rng));
+        const float psi2 = rnd(rng);
+        const float alpha = 1.0f - psi1;
+        const float beta = (1.0f - psi2) * psi1;
+        const float gamma = psi2 * psi1;
+        point = add(add(muls(v0, alpha), muls(v1, beta)), muls(v2, gamma));
+    } else {
+        point = divs(add(add(v0, v1), v2), 3.0f);
+    }
+    const f3 normal = normalize(cross(sub(v0, v1), sub(v0, v2)));
+    const f3 ld = sub(point, pos);
+    const float cos_l = dot(normalize(neg(ld)), normal);
+    const float distance = rt_det_sqrtf(dot(ld, ld));
+    Light L;
+    L.l_i = muls(muls(l_e, area), cos_l);
+    if (MODE == RT_MODE_W7E2) L.l_i = divs(L.l_i, distance * distance);
+    L.w_i = normalize(ld);
+    L.dist = distance;
+    return L;
+}
+
+template <int MODE, int TRAV, bool COUNT>
+__device__ __forceinline__ f3 direct_sample(const DevScene& S, void* stk, const BvhDeep& dp, const f3 ro,
+                                            const f3 rd, uint32_t& rng, uint32_t& prim, Counters& cnt)
+{
+    constexpr bool W6 = MODE == RT_MODE_W6E2, E2 = MODE == RT_MODE_W7E2;
+    const float ETA = W6 ? 0.00001f : 0.001f;
+    cnt.v[C_PRIMARY]++;
+    TraceOut tr;
+    if (!trace<TRAV, COUNT>(S, stk, dp, ro, rd, ETA, 5000.0f, false, tr, cnt))
+        return W6 ? V(0.1f, 0.3f, 0.6f) : V(0.0f, 0.0f, 0.0f);   // result += bgcolor.rgb
+    const HitRec h = resolve<TRAV>(S, tr, ro, rd, true);
+    prim = h.tri;
+    // lambertian: w6e2.wgsl:297-322 / w7e1.wgsl:385-410 / w7e2.wgsl:392-417
+    const rt_material& m = mat_of(S, h.material);
+    const f3 bdrf = ld3(m.diffuse);
+    f3 diffuse = V(0, 0, 0);
+    for (uint32_t idx = 1; idx < S.nlights; idx++) {
+        const Light Lt = direct_light<MODE>(S, h.pos, idx, rng);
+        const f3 so = E2 ? h.pos : add(h.pos, muls(muls(h.nrm, ETA), W6 ? 10.0f : 100.0f));
+        const float stmax = E2 ? Lt.dist - ETA : Lt.dist - ETA * 1000.0f;
+        cnt.v[C_SHADOW]++;
+        TraceOut sh;
+        if (trace<TRAV, COUNT>(S, stk, dp, so, Lt.w_i, ETA, stmax, true, sh, cnt)) continue;   // blocked
+        const float dd = dot(h.nrm, Lt.w_i);
+        if (E2) {
+            diffuse = add(diffuse, divs(mul(mul(bdrf, V(dd, dd, dd)), Lt.l_i), RT_PI_F));
+        } else {   // light_diffuse_contribution
+            f3 c = divs(V(dd, dd, dd), Lt.dist * Lt.dist);
+            c = mul(c, Lt.l_i);
+            c = divs(c, RT_PI_F);
+            diffuse = add(diffuse, mul(bdrf, c));
+        }
+    }
+    if (E2) return add(diffuse, ld3(m.ambient));
+    const f3 ambient = add(ld3(m.ambient), muls(ld3(m.diffuse), 0.1f));
+    return add(muls(diffuse, 0.9f), muls(ambient, 0.1f));   // diffuse_and_ambient
+}
+
+template <int MODE, int TRAV, bool COUNT>
+__global__ void __launch_bounds__(256) k_direct(DevScene S, DevLaunch L)
+{
+    extern __shared__ uint32_t lds_stack[];
+    void* stk = TRAV == RT_TRAVERSE_BVH ? lds_stack + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u)
+                                        : lds_stack + threadIdx.x;
+    const BvhDeep dp{TRAV == RT_TRAVERSE_BVH ? L.bvh_deep + (size_t)blockIdx.x * 256u + threadIdx.x : nullptr,
+                     gridDim.x * 256u};
+    const uint32_t lane = threadIdx.x & 63u;
+    const Cam cam = make_cam(L);
+    Counters cnt;
+#pragma unroll
+    for (int i = 0; i < C_N; i++) cnt.v[i] = 0;
+    for (;;) {
+        const uint32_t work = fetch_work(L.work_counter, lane);
+        if (work >= L.nwork) break;
+        const Pix px = map_pixel(L, work, lane);
+        if (!px.valid) continue;
+        float ux, uy;
+        pixel_uv(L.u, px.x, px.y, ux, uy);
+        uint32_t prim = 0xFFFFFFFFu;
+        if (MODE == RT_MODE_W6E2) {
+            // fs_main, w6e2.wgsl:160-186
+            const uint32_t subdiv = L.u.subdivision_level, nsamp = subdiv * subdiv;
+            f3 res = V(0, 0, 0);
+            uint32_t rng = 0;
+            cnt.v[C_SAMPLES]++;
+            for (uint32_t s = 0; s < nsamp; s++) {
+                const float jx = L.jitter ? L.jitter[2u * s] : 0.0f;
+                const float jy = L.jitter ? L.jitter[2u * s + 1u] : 0.0f;
+                uint32_t p = 0xFFFFFFFFu;
+                res = add(res, direct_sample<MODE, TRAV, COUNT>(S, stk, dp, cam.e, cam_dir(cam, ux, uy, jx, jy), rng, p,
+                                                                cnt));
+                if (s + 1u == nsamp) prim = p;
+            }
+            res = muls(res, 1.0f / (float)nsamp);
+            L.accum[px.out] = make_float4(res.x, res.y, res.z, 1.0f);
+        } else {
+            // fs_main, w7e1.wgsl:202-236: iterations in order, folded as the shader does
+            float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f;
+            if (L.first_iter > 0u) {
+                const float4 pa = L.accum[px.out];
+                a0 = pa.x;
+                a1 = pa.y;
+                a2 = pa.z;
+            }
+            const float fH = (float)L.u.resolution[1];
+            for (uint32_t k = 0; k < L.spp; k++) {
+                const uint32_t it = L.first_iter + k;
+                uint32_t rng = tea16(px.y * L.u.resolution[0] + px.x, it);
+                float jx = rnd(rng);
+                float jy = rnd(rng);
+                jx = jx / fH;
+                jy = jy / fH;
+                cnt.v[C_SAMPLES]++;
+                prim = 0xFFFFFFFFu;
+                const f3 r = direct_sample<MODE, TRAV, COUNT>(S, stk, dp, cam.e, cam_dir(cam, ux, uy, jx, jy), rng, prim,
+                                                              cnt);
+                const float fi = (float)it, fi1 = (float)(it + 1u);
+                a0 = (r.x + a0 * fi) / fi1;
+                a1 = (r.y + a1 * fi) / fi1;
+                a2 = (r.z + a2 * fi) / fi1;
+            }
+            L.accum[px.out] = make_float4(a0, a1, a2, 1.0f);
+        }
+        if (L.ids) L.ids[px.out] = prim;
+    }
+    flush_counters(cnt, L.counters, COUNT);
+}
+
 // ------------------------------------------------------------------ W1E6 analytic kernel
 // res/shaders/w1e6.wgsl: triangle + sphere + plane, point light, no mesh.
 __device__ __forceinline__ bool w1_triangle(f3 o, f3 w, float tmin, float& tmax, f3 a, f3 b, f3 c, f3& pos,
@@ -1631,6 +1781,11 @@ static void launch_path(const DevScene& s, const DevLaunch& l, int grid, size_t 
 {
     hipLaunchKernelGGL((k_path<MODE, TRAV, COUNT>), dim3(grid), dim3(256), lds, st, s, l);
 }
+template <int MODE, int TRAV, bool COUNT>
+static void launch_direct(const DevScene& s, const DevLaunch& l, int grid, size_t lds, hipStream_t st)
+{
+    hipLaunchKernelGGL((k_direct<MODE, TRAV, COUNT>), dim3(grid), dim3(256), lds, st, s, l);
+}
 template <int TRAV, bool COUNT>
 static void launch_primary(const DevScene& s, const DevLaunch& l, int project, int grid, size_t lds, hipStream_t st)
 {
@@ -1697,6 +1852,24 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
                         : launch_path<RT_MODE_W8E3, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
         else detail ? launch_path<RT_MODE_W8E3, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
                     : launch_path<RT_MODE_W8E3, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        break;
+    case RT_MODE_W6E2:
+        if (bvh) detail ? launch_direct<RT_MODE_W6E2, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_direct<RT_MODE_W6E2, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_direct<RT_MODE_W6E2, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_direct<RT_MODE_W6E2, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        break;
+    case RT_MODE_W7E1:
+        if (bvh) detail ? launch_direct<RT_MODE_W7E1, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_direct<RT_MODE_W7E1, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_direct<RT_MODE_W7E1, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_direct<RT_MODE_W7E1, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        break;
+    case RT_MODE_W7E2:
+        if (bvh) detail ? launch_direct<RT_MODE_W7E2, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_direct<RT_MODE_W7E2, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_direct<RT_MODE_W7E2, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_direct<RT_MODE_W7E2, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         break;
     case RT_MODE_W6E1:
     case RT_MODE_PROJECT: {

@@ -107,6 +107,9 @@ std::optional<rt_mode> SceneDescriptor::mode() const
     if (shader == "w8e2.wgsl") return RT_MODE_W8E2;
     if (shader == "w8e3.wgsl") return RT_MODE_W8E3;
     if (shader == "w9e2.wgsl") return RT_MODE_W9E2;
+    if (shader == "w6e2.wgsl") return RT_MODE_W6E2;
+    if (shader == "w7e1.wgsl") return RT_MODE_W7E1;
+    if (shader == "w7e2.wgsl") return RT_MODE_W7E2;
     return std::nullopt;
 }
 
@@ -384,7 +387,8 @@ void RenderState::render(uint32_t spp)
                          static_cast<uint32_t*>(ids_), nullptr),
                "render");
     const bool path = mode_ == RT_MODE_W7E3 || mode_ == RT_MODE_W9E1 || mode_ == RT_MODE_W8E1 ||
-                      mode_ == RT_MODE_W8E2 || mode_ == RT_MODE_W8E3 || mode_ == RT_MODE_W9E2;
+                      mode_ == RT_MODE_W8E2 || mode_ == RT_MODE_W8E3 || mode_ == RT_MODE_W9E2 ||
+                      mode_ == RT_MODE_W7E1 || mode_ == RT_MODE_W7E2;
     if (progressive_ && path) iteration_ += spp;
     update();
 }

@@ -64,6 +64,9 @@ static const char* mode_name(std::optional<rt_mode> m)
     case RT_MODE_W8E2: return "W8E2";
     case RT_MODE_W8E3: return "W8E3";
     case RT_MODE_W9E2: return "W9E2";
+    case RT_MODE_W6E2: return "W6E2";
+    case RT_MODE_W7E1: return "W7E1";
+    case RT_MODE_W7E2: return "W7E2";
     }
     return nullptr;
 }

@@ -19,6 +19,9 @@ SHADER_MODES = {
     "w8e2.wgsl": "W8E2",
     "w8e3.wgsl": "W8E3",
     "w9e2.wgsl": "W9E2",
+    "w6e2.wgsl": "W6E2",
+    "w7e1.wgsl": "W7E1",
+    "w7e2.wgsl": "W7E2",
 }
 
 

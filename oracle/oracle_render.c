@@ -944,6 +944,145 @@ static void sample_w6e1(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, float ou
     out[2] = result.z;
 }
 
+/* ------------------------------------------------------------ W6E2 / W7E1 / W7E2
+ * Cornell-box direct lighting (res/shaders/w6e2.wgsl, w7e1.wgsl, w7e2.wgsl):
+ * one closest-hit ray per sample, then a shadow ray to every area-light
+ * triangle; W6E2 takes subdiv^2 jittered samples, W7E1/W7E2 are progressive. */
+static Light area_light_direct(Ctx* C, v3 pos, uint32_t idx, uint32_t* t)
+{
+    /* sample_area_light: w6e2.wgsl:245-262 / w7e1.wgsl:327-346 (triangle
+     * centre, l_i without 1/d^2) and w7e2.wgsl:327-354 (random point, 1/d^2);
+     * cos_l is not clamped in any of the three */
+    const or_scene* s = C->s;
+    uint32_t li = s->lights[idx < s->nlights ? idx : s->nlights - 1];
+    const uint32_t* tri = s->idx + 4 * (size_t)(li < s->ntris ? li : s->ntris - 1);
+    v3 v0 = load3(s->pos + 4 * (size_t)tri[0]);
+    v3 v1 = load3(s->pos + 4 * (size_t)tri[1]);
+    v3 v2 = load3(s->pos + 4 * (size_t)tri[2]);
+    float area = triangle_area(v0, v1, v2);
+    v3 l_e = load3(mat_of(s, tri[3])->ambient);
+    v3 point;
+    if (C->mode == OR_MODE_W7E2) {
+        float psi1 = rt_det_sqrtf(rnd(t));
+        float psi2 = rnd(t);
+        float alpha = 1.0f - psi1;
+        float beta = (1.0f - psi2) * psi1;
+        float gamma = psi2 * psi1;
+        point = add(add(muls(v0, alpha), muls(v1, beta)), muls(v2, gamma));
+    } else {
+        point = divs(add(add(v0, v1), v2), 3.0f);
+    }
+    v3 normal = normalize(cross(sub(v0, v1), sub(v0, v2)));
+    v3 ld = sub(point, pos);
+    float cos_l = dot(normalize(neg(ld)), normal);
+    float distance = rt_det_sqrtf(dot(ld, ld));
+    Light L;
+    L.l_i = muls(muls(l_e, area), cos_l);
+    if (C->mode == OR_MODE_W7E2) L.l_i = divs(L.l_i, distance * distance);
+    L.w_i = normalize(ld);
+    L.dist = distance;
+    return L;
+}
+
+static v3 lambertian_direct(Ctx* C, Hit* h, uint32_t* t)
+{
+    /* w6e2.wgsl:297-322 / w7e1.wgsl:385-410 / w7e2.wgsl:392-417 */
+    const or_scene* s = C->s;
+    const int e2 = C->mode == OR_MODE_W7E2;
+    const float ETA = C->mode == OR_MODE_W6E2 ? 0.00001f : 0.001f;
+    const float off = C->mode == OR_MODE_W6E2 ? 10.0f : 100.0f;
+    v3 normal = h->normal, position = h->position;
+    const or_material* m = mat_of(s, h->material);
+    v3 bdrf = load3(m->diffuse);
+    v3 diffuse = V(0, 0, 0);
+    for (uint32_t idx = 1; idx < s->nlights; idx++) {
+        Light L = area_light_direct(C, position, idx, t);
+        Ray sr;
+        sr.direction = L.w_i;
+        sr.origin = e2 ? position : add(position, muls(muls(normal, ETA), off));
+        sr.tmin = ETA;
+        sr.tmax = e2 ? L.dist - ETA : L.dist - ETA * 1000.0f;
+        Hit hi;
+        memset(&hi, 0, sizeof hi);
+        C->c.shadow++;
+        if (trace(C, &sr, &hi, 1)) continue;   /* blocked */
+        float dd = dot(normal, L.w_i);
+        if (e2) {
+            diffuse = add(diffuse, divs(mul(mul(bdrf, V(dd, dd, dd)), L.l_i), PI_F));
+        } else {   /* light_diffuse_contribution */
+            v3 c = divs(V(dd, dd, dd), L.dist * L.dist);
+            c = mul(c, L.l_i);
+            c = divs(c, PI_F);
+            diffuse = add(diffuse, mul(bdrf, c));
+        }
+    }
+    if (e2) return add(diffuse, load3(m->ambient));
+    v3 ambient = add(load3(m->ambient), muls(load3(m->diffuse), 0.1f));
+    return add(muls(diffuse, 0.9f), muls(ambient, 0.1f));   /* diffuse_and_ambient */
+}
+
+static v3 trace_direct(Ctx* C, Ray* r, uint32_t* t, uint32_t* prim, int record_prim)
+{
+    /* one sample of fs_main: the shader is always LAMBERTIAN, which ends the
+     * bounce loop (has_hit) */
+    v3 bg = C->mode == OR_MODE_W6E2 ? V(0.1f, 0.3f, 0.6f) : V(0.0f, 0.0f, 0.0f);
+    Hit h;
+    memset(&h, 0, sizeof h);
+    C->c.primary++;
+    if (!trace(C, r, &h, 1)) return bg;
+    if (record_prim) *prim = h.tri;
+    return lambertian_direct(C, &h, t);
+}
+
+static void sample_w6e2(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, float out[3], uint32_t* prim)
+{
+    /* fs_main, w6e2.wgsl:160-186: subdiv^2 jittered samples, averaged */
+    const or_uniform* u = C->u;
+    uint32_t subdiv = u->subdivision_level;
+    v3 result = V(0, 0, 0);
+    float ux, uy;
+    pixel_uv(u, x, y, &ux, &uy);
+    *prim = 0xFFFFFFFFu;
+    for (uint32_t sample = 0; sample < subdiv * subdiv; sample++) {
+        float jx = C->jitter ? C->jitter[2 * sample] : 0.0f;
+        float jy = C->jitter ? C->jitter[2 * sample + 1] : 0.0f;
+        Ray r;
+        r.direction = cam_dir(cam, ux, uy, jx, jy);
+        r.origin = cam->e;
+        r.tmax = 5000.0f;
+        r.tmin = 0.00001f;
+        result = add(result, trace_direct(C, &r, NULL, prim, sample + 1 == subdiv * subdiv));
+    }
+    result = muls(result, 1.0f / (float)(subdiv * subdiv));
+    out[0] = result.x;
+    out[1] = result.y;
+    out[2] = result.z;
+}
+
+static void sample_w7_direct(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t it, float out[3],
+                             uint32_t* prim)
+{
+    /* fs_main, w7e1.wgsl:202-236 / w7e2.wgsl: TEA-seeded jitter, one sample */
+    const or_uniform* u = C->u;
+    uint32_t t = tea16(y * u->resolution[0] + x, it);
+    float jx = rnd(&t);
+    float jy = rnd(&t);
+    jx = jx / (float)u->resolution[1];
+    jy = jy / (float)u->resolution[1];
+    float ux, uy;
+    pixel_uv(u, x, y, &ux, &uy);
+    Ray r;
+    r.direction = cam_dir(cam, ux, uy, jx, jy);
+    r.origin = cam->e;
+    r.tmax = 5000.0f;
+    r.tmin = 0.001f;
+    *prim = 0xFFFFFFFFu;
+    v3 res = trace_direct(C, &r, &t, prim, 1);
+    out[0] = res.x;
+    out[1] = res.y;
+    out[2] = res.z;
+}
+
 /* ------------------------------------------------------------ W1E6 */
 
 static int w1_triangle(Ray* r, Hit* h, v3 a, v3 b, v3 c)   /* w1e6.wgsl:179-209 */
@@ -1080,7 +1219,9 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
         size_t o = (size_t)ry * J->w + rx;
         float* acc = J->accum + 4 * o;
         uint32_t prim = 0xFFFFFFFFu;
-        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 || J->mode >= OR_MODE_W8E1) {   /* progressive */
+        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 || (J->mode >= OR_MODE_W8E1 && J->mode != OR_MODE_W6E2)) {
+            /* progressive */
+            const int clamp0 = J->mode != OR_MODE_W7E1 && J->mode != OR_MODE_W7E2;   /* w7e1.wgsl:229-235: no max */
             float a[3] = {acc[0], acc[1], acc[2]};
             if (J->first_iter == 0) a[0] = a[1] = a[2] = 0.0f;
             for (uint32_t k = 0; k < J->spp; k++) {
@@ -1088,12 +1229,13 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
                 float res[3];
                 C->c.samples++;
                 if (J->mode >= OR_MODE_W8E1 && J->mode <= OR_MODE_W8E3) sample_w8(C, cam, x, y, it, res, &prim);
+                else if (J->mode == OR_MODE_W7E1 || J->mode == OR_MODE_W7E2) sample_w7_direct(C, cam, x, y, it, res, &prim);
                 else sample_path(C, cam, x, y, it, res, &prim);
                 /* fs_main accumulation, w7e3.wgsl:261-271 */
                 for (int c = 0; c < 3; c++) {
                     float curr_sum = a[c] * (float)it;
                     float ac = (res[c] + curr_sum) / (float)(it + 1u);
-                    a[c] = rt_max0f(ac);
+                    a[c] = clamp0 ? rt_max0f(ac) : ac;
                 }
             }
             acc[0] = a[0]; acc[1] = a[1]; acc[2] = a[2]; acc[3] = 1.0f;
@@ -1101,6 +1243,7 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
             float res[3];
             C->c.samples++;
             if (J->mode == OR_MODE_W1E6) sample_w1e6(C, cam, x, y, res, &prim);
+            else if (J->mode == OR_MODE_W6E2) sample_w6e2(C, cam, x, y, res, &prim);
             else sample_w6e1(C, cam, x, y, res, &prim);
             acc[0] = res[0]; acc[1] = res[1]; acc[2] = res[2]; acc[3] = 1.0f;
         }
@@ -1136,7 +1279,7 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
               uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
               float* accum, uint32_t* ids, or_counts* counts, int nthreads)
 {
-    if (mode < 0 || mode > OR_MODE_W9E2) return -1;
+    if (mode < 0 || mode > OR_MODE_W7E2) return -1;
     if (mode != OR_MODE_W1E6) {
         if (!s || !s->nmats) return -1;
         if (trav == OR_TRAV_BSP && (!s->tree || !s->planes)) return -1;
