@@ -778,7 +778,7 @@ int rt_set_environment_map(rt_ctx* c, const uint8_t* rgba8, uint32_t width, uint
 static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
 {
     if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
-    if (mode < RT_MODE_W1E6 || mode > RT_MODE_W7E2) return fail(c, RT_E_INVALID, "rt_render: bad mode");
+    if (mode < RT_MODE_W1E6 || mode > RT_MODE_W6E3) return fail(c, RT_E_INVALID, "rt_render: bad mode");
     // W7E1/W7E2: progressive, folded inside k_direct (no per-iteration samples)
     const bool direct_prog = mode == RT_MODE_W7E1 || mode == RT_MODE_W7E2;
     // progressive path tracers: per-iteration samples, folded in order by k_fold

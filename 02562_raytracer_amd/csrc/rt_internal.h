@@ -129,6 +129,6 @@ void camera_basis(const rt_uniform& u, float cam[14]);
 // Host reference of the pinned math for the self test (same header, host compile).
 void host_math(const float* in, float* out, uint32_t n);
 
-constexpr int kMathOuts = 14;   // outputs per input in the math self test
+constexpr int kMathOuts = 16;   // outputs per input in the math self test
 
 }  // namespace rtk

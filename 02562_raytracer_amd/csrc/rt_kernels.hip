@@ -1442,7 +1442,8 @@ __device__ __forceinline__ Light direct_light(const DevScene& S, f3 pos, uint32_
     const float distance = rt_det_sqrtf(dot(ld, ld));
     Light L;
     L.l_i = muls(muls(l_e, area), cos_l);
-    if (MODE == RT_MODE_W7E2) L.l_i = divs(L.l_i, distance * distance);
+    // W6E3 (w6e3.wgsl:298-318): the centre, with 1/d^2
+    if (MODE == RT_MODE_W7E2 || MODE == RT_MODE_W6E3) L.l_i = divs(L.l_i, distance * distance);
     L.w_i = normalize(ld);
     L.dist = distance;
     return L;
@@ -1486,6 +1487,93 @@ __device__ __forceinline__ f3 direct_sample(const DevScene& S, void* stk, const 
     return add(muls(diffuse, 0.9f), muls(ambient, 0.1f));   // diffuse_and_ambient
 }
 
+// One sample of w6e3.wgsl's fs_main (:166-192): up to MAX_DEPTH 10 segments
+// through intersect_scene_bsp (mirror ball, glossy ball with ior 1.5, then the
+// mesh, :196-216).  Lambertian ends the sample; the mirror reflects from the
+// hit point; glossy adds the Phong lobe over all lights and refracts
+// (transmit), or ends with error_shader() under total internal reflection.
+// `result` is fs_main's running sum over all samples and segments (the
+// shader adds every segment's shade() to it in order).
+template <int TRAV, bool COUNT>
+__device__ __forceinline__ void w6e3_sample(const DevScene& S, const DevLaunch& L, void* stk, const BvhDeep& dp,
+                                            f3 ro, f3 rd, uint32_t& prim, Counters& cnt, f3& result)
+{
+    const float ETA = 0.001f;
+    uint32_t rng = 0;
+    cnt.v[C_PRIMARY]++;
+    for (int i = 0; i < 10; i++) {
+        if (i > 0) cnt.v[C_BOUNCE]++;
+        const W8Ball b = w8_balls(ro, rd, ETA, 5000.0f);
+        TraceOut tr;
+        if (trace<TRAV, COUNT>(S, stk, dp, ro, rd, ETA, b.t, false, tr, cnt)) {
+            // lambertian, w6e3.wgsl:354-379
+            const HitRec h = resolve<TRAV>(S, tr, ro, rd, true);
+            if (i == 0) prim = h.tri;
+            const rt_material& m = mat_of(S, h.material);
+            const f3 bdrf = ld3(m.diffuse);
+            f3 diffuse = V(0, 0, 0);
+            for (uint32_t idx = 1; idx < S.nlights; idx++) {
+                const Light Lt = direct_light<RT_MODE_W6E3>(S, h.pos, idx, rng);
+                cnt.v[C_SHADOW]++;
+                if (w8_balls(h.pos, Lt.w_i, ETA, Lt.dist - ETA).id != 0u) continue;   // a ball blocks
+                TraceOut sh;
+                if (trace<TRAV, COUNT>(S, stk, dp, h.pos, Lt.w_i, ETA, Lt.dist - ETA, true, sh, cnt)) continue;
+                const float dd = dot(h.nrm, Lt.w_i);
+                diffuse = add(diffuse, divs(mul(mul(bdrf, V(dd, dd, dd)), Lt.l_i), RT_PI_F));
+            }
+            result = add(result, add(diffuse, ld3(m.ambient)));
+            break;
+        }
+        if (b.id == 1u) {
+            // mirror, w6e3.wgsl:381-389: origin at the hit point
+            rd = sub(rd, muls(b.nrm, 2.0f * dot(b.nrm, rd)));
+            ro = b.pos;
+            result = add(result, V(0, 0, 0));
+            continue;
+        }
+        if (b.id == 2u) {
+            // glossy = phong + transmit, w6e3.wgsl:391-457
+            const f3 normal = b.nrm, position = b.pos;
+            const float coeff = 0.9f * (42.0f + 2.0f) / (2.0f * RT_PI_F);
+            const f3 w_o = normalize(sub(V(L.u.camera_pos[0], L.u.camera_pos[1], L.u.camera_pos[2]), position));
+            f3 phong_total = V(0, 0, 0);
+            for (uint32_t idx = 1; idx < S.nlights; idx++) {
+                const Light Lt = direct_light<RT_MODE_W6E3>(S, position, idx, rng);
+                const f3 nw = neg(Lt.w_i);
+                const f3 w_r = normalize(sub(nw, muls(normal, 2.0f * dot(normal, nw))));
+                const float dd = rt_satf(dot(normal, Lt.w_i));
+                const f3 dif = divs(mul(V(dd, dd, dd), Lt.l_i), RT_PI_F);
+                phong_total = add(phong_total, muls(dif, rt_det_powf(rt_satf(dot(w_o, w_r)), 42.0f)));
+            }
+            const f3 ph = muls(phong_total, coeff);
+            // transmit
+            const f3 w_i = neg(normalize(rd));
+            const f3 n2 = normalize(normal);
+            float ior = 1.5f;
+            const float cos_i = dot(w_i, n2);
+            f3 out_n;
+            if (cos_i < 0.0f) {
+                out_n = neg(n2);
+            } else {
+                ior = 1.0f / ior;
+                out_n = n2;
+            }
+            const float cos_t2 = (1.0f - (ior * ior) * (1.0f - cos_i * cos_i));
+            if (cos_t2 < 0.0f) {   // error_shader(); has_hit stays set
+                result = add(result, add(ph, V(0.7f, 0.0f, 0.7f)));
+                break;
+            }
+            const f3 tangent = sub(muls(n2, cos_i), w_i);
+            rd = sub(muls(tangent, ior), muls(out_n, rt_det_sqrtf(cos_t2)));
+            ro = position;
+            result = add(result, add(ph, V(0, 0, 0)));
+            continue;
+        }
+        result = add(result, V(0, 0, 0));   // BACKGROUND_COLOR (0, 0, 0)
+        break;
+    }
+}
+
 template <int MODE, int TRAV, bool COUNT>
 __global__ void __launch_bounds__(256) k_direct(DevScene S, DevLaunch L)
 {
@@ -1507,8 +1595,8 @@ __global__ void __launch_bounds__(256) k_direct(DevScene S, DevLaunch L)
         float ux, uy;
         pixel_uv(L.u, px.x, px.y, ux, uy);
         uint32_t prim = 0xFFFFFFFFu;
-        if (MODE == RT_MODE_W6E2) {
-            // fs_main, w6e2.wgsl:160-186
+        if (MODE == RT_MODE_W6E2 || MODE == RT_MODE_W6E3) {
+            // fs_main, w6e2.wgsl:160-186 / w6e3.wgsl:166-192
             const uint32_t subdiv = L.u.subdivision_level, nsamp = subdiv * subdiv;
             f3 res = V(0, 0, 0);
             uint32_t rng = 0;
@@ -1517,8 +1605,9 @@ __global__ void __launch_bounds__(256) k_direct(DevScene S, DevLaunch L)
                 const float jx = L.jitter ? L.jitter[2u * s] : 0.0f;
                 const float jy = L.jitter ? L.jitter[2u * s + 1u] : 0.0f;
                 uint32_t p = 0xFFFFFFFFu;
-                res = add(res, direct_sample<MODE, TRAV, COUNT>(S, stk, dp, cam.e, cam_dir(cam, ux, uy, jx, jy), rng, p,
-                                                                cnt));
+                const f3 rd0 = cam_dir(cam, ux, uy, jx, jy);
+                if (MODE == RT_MODE_W6E3) w6e3_sample<TRAV, COUNT>(S, L, stk, dp, cam.e, rd0, p, cnt, res);
+                else res = add(res, direct_sample<MODE, TRAV, COUNT>(S, stk, dp, cam.e, rd0, rng, p, cnt));
                 if (s + 1u == nsamp) prim = p;
             }
             res = muls(res, 1.0f / (float)nsamp);
@@ -1727,6 +1816,8 @@ __host__ __device__ inline void math_eval(float x, float* o)
     o[11] = rt_det_atanf(x * 5.0f);
     o[12] = rt_det_expf(x * 30.0f);    // over- and underflow at |x| > 2.96 / 3.47
     o[13] = rt_det_exp2f(x * 40.0f);   // the RGBE decode's pow(2, e) (w9e2.wgsl:244); subnormal below -126
+    o[14] = rt_det_powf(rt_satf(x * 0.3f + 0.5f), 42.0f);   // the phong lobe pow(saturate(.), 42) (w6e3.wgsl:418)
+    o[15] = rt_det_log2f(x < 0.0f ? -x * 1e-30f : x * 1e30f);
 }
 __global__ void k_selftest_math(const float* in, float* out, uint32_t n)
 {
@@ -1858,6 +1949,12 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
                         : launch_direct<RT_MODE_W6E2, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
         else detail ? launch_direct<RT_MODE_W6E2, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
                     : launch_direct<RT_MODE_W6E2, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
+        break;
+    case RT_MODE_W6E3:
+        if (bvh) detail ? launch_direct<RT_MODE_W6E3, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_direct<RT_MODE_W6E3, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_direct<RT_MODE_W6E3, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_direct<RT_MODE_W6E3, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         break;
     case RT_MODE_W7E1:
         if (bvh) detail ? launch_direct<RT_MODE_W7E1, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)

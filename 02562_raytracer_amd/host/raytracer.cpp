@@ -110,6 +110,7 @@ std::optional<rt_mode> SceneDescriptor::mode() const
     if (shader == "w6e2.wgsl") return RT_MODE_W6E2;
     if (shader == "w7e1.wgsl") return RT_MODE_W7E1;
     if (shader == "w7e2.wgsl") return RT_MODE_W7E2;
+    if (shader == "w6e3.wgsl") return RT_MODE_W6E3;
     return std::nullopt;
 }
 

@@ -22,6 +22,7 @@ SHADER_MODES = {
     "w6e2.wgsl": "W6E2",
     "w7e1.wgsl": "W7E1",
     "w7e2.wgsl": "W7E2",
+    "w6e3.wgsl": "W6E3",
 }
 
 

@@ -179,6 +179,40 @@ RT_HD float rt_det_exp2f(float x)
     return __builtin_ldexpf(__builtin_ldexpf(px, n1), n2);
 }
 
+/* log2: Cephes log2f (frexp split about sqrt(1/2), degree-9 polynomial,
+ * log2(e) applied in two parts); log2(0) = -inf, negative or NaN -> NaN. */
+RT_HD float rt_det_log2f(float xx)
+{
+    if (xx != xx || xx < 0.0f) return __builtin_nanf("");
+    if (xx == 0.0f) return -__builtin_inff();
+    if (xx == __builtin_inff()) return xx;
+    int e;
+    float x = __builtin_frexpf(xx, &e);
+    if (x < 0.707106781186547524f) {
+        e -= 1;
+        x = x + x - 1.0f;
+    } else {
+        x = x - 1.0f;
+    }
+    const float z = x * x;
+    float y = ((((((((7.0376836292e-2f * x - 1.1514610310e-1f) * x + 1.1676998740e-1f) * x - 1.2420140846e-1f) * x
+                   + 1.4249322787e-1f) * x - 1.6668057665e-1f) * x + 2.0000714765e-1f) * x - 2.4999993993e-1f) * x
+              + 3.3333331174e-1f) * x * z;
+    y = y + -0.5f * z;
+    float r = y * 0.44269504088896340736f;
+    r = r + x * 0.44269504088896340736f;
+    r = r + y;
+    r = r + x;
+    return r + (float)e;
+}
+
+/* WGSL pow(x, y) = exp2(y * log2(x)) for x >= 0 (the phong lobe, w6e3.wgsl:418) */
+RT_HD float rt_det_powf(float x, float y)
+{
+    if (x == 0.0f) return y > 0.0f ? 0.0f : (y == 0.0f ? 1.0f : __builtin_inff());
+    return rt_det_exp2f(y * rt_det_log2f(x));
+}
+
 /* atan on |x| <= tan(pi/8) after the Cephes atanf reduction */
 RT_HD float rt_det_atanf(float x)
 {

@@ -978,7 +978,7 @@ static Light area_light_direct(Ctx* C, v3 pos, uint32_t idx, uint32_t* t)
     float distance = rt_det_sqrtf(dot(ld, ld));
     Light L;
     L.l_i = muls(muls(l_e, area), cos_l);
-    if (C->mode == OR_MODE_W7E2) L.l_i = divs(L.l_i, distance * distance);
+    if (C->mode == OR_MODE_W7E2 || C->mode == OR_MODE_W6E3) L.l_i = divs(L.l_i, distance * distance);
     L.w_i = normalize(ld);
     L.dist = distance;
     return L;
@@ -1081,6 +1081,137 @@ static void sample_w7_direct(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uin
     out[0] = res.x;
     out[1] = res.y;
     out[2] = res.z;
+}
+
+/* ------------------------------------------------------------ W6E3
+ * res/shaders/w6e3.wgsl: W6E2's scene loop over the Cornell box with the two
+ * balls of intersect_scene_bsp (:196-216): mirror, glossy (phong + transmit,
+ * ior 1.5), lambertian mesh with 1/d^2 centre lights. */
+static int intersect_scene_w6e3(Ctx* C, Ray* r, Hit* h)
+{
+    int has_hit = 0;
+    if (intersect_sphere(r, h, V(420.0f, 90.0f, 370.0f), 90.0f)) {
+        h->shader = 2;
+        has_hit = 1;
+    }
+    if (intersect_sphere(r, h, V(130.0f, 90.0f, 250.0f), 90.0f)) {
+        h->shader = 4;   /* GLOSSY, ior1_over_ior2 = 1.5 */
+        has_hit = 1;
+    }
+    if (trace(C, r, h, 1)) {
+        h->shader = 0;
+        has_hit = 1;
+    }
+    return has_hit;
+}
+
+static v3 shade_w6e3(Ctx* C, Ray* r, Hit* h)
+{
+    const or_scene* s = C->s;
+    const float ETA = 0.001f;
+    h->has_hit = 1;
+    if (h->shader == 0) {   /* lambertian, :354-379 */
+        v3 normal = h->normal;
+        const or_material* m = mat_of(s, h->material);
+        v3 bdrf = load3(m->diffuse);
+        v3 diffuse = V(0, 0, 0);
+        for (uint32_t idx = 1; idx < s->nlights; idx++) {
+            Light L = area_light_direct(C, h->position, idx, NULL);
+            Ray sr;
+            sr.direction = L.w_i;
+            sr.origin = h->position;
+            sr.tmax = L.dist - ETA;
+            sr.tmin = ETA;
+            Hit hi;
+            memset(&hi, 0, sizeof hi);
+            C->c.shadow++;
+            if (intersect_scene_w6e3(C, &sr, &hi)) continue;
+            float dd = dot(normal, L.w_i);
+            diffuse = add(diffuse, divs(mul(mul(bdrf, V(dd, dd, dd)), L.l_i), PI_F));
+        }
+        return add(diffuse, load3(m->ambient));
+    }
+    if (h->shader == 2) {   /* mirror, :381-389 */
+        v3 n = h->normal, d = r->direction;
+        r->direction = sub(d, muls(n, 2.0f * dot(n, d)));
+        r->origin = h->position;
+        r->tmax = 5000.0f;
+        r->tmin = ETA;
+        h->has_hit = 0;
+        return V(0, 0, 0);
+    }
+    /* glossy = phong + transmit, :391-457 */
+    v3 normal = h->normal, position = h->position;
+    float coeff = 0.9f * (42.0f + 2.0f) / (2.0f * PI_F);
+    v3 w_o = normalize(sub(load3(C->u->camera_pos), position));
+    v3 phong_total = V(0, 0, 0);
+    for (uint32_t idx = 1; idx < s->nlights; idx++) {
+        Light L = area_light_direct(C, position, idx, NULL);
+        v3 nw = neg(L.w_i);
+        v3 w_r = normalize(sub(nw, muls(normal, 2.0f * dot(normal, nw))));
+        float dd = rt_satf(dot(normal, L.w_i));
+        v3 dif = divs(mul(V(dd, dd, dd), L.l_i), PI_F);
+        phong_total = add(phong_total, muls(dif, rt_det_powf(rt_satf(dot(w_o, w_r)), 42.0f)));
+    }
+    v3 ph = muls(phong_total, coeff);
+    v3 w_i = neg(normalize(r->direction));
+    v3 n2 = normalize(h->normal);
+    float ior = 1.5f;
+    float cos_i = dot(w_i, n2);
+    v3 out_n;
+    if (cos_i < 0.0f) {
+        out_n = neg(n2);
+    } else {
+        ior = 1.0f / ior;
+        out_n = n2;
+    }
+    float cos_t2 = (1.0f - (ior * ior) * (1.0f - cos_i * cos_i));
+    if (cos_t2 < 0.0f) return add(ph, V(0.7f, 0.0f, 0.7f));   /* error_shader, has_hit stays */
+    v3 tangent = sub(muls(n2, cos_i), w_i);
+    r->direction = sub(muls(tangent, ior), muls(out_n, rt_det_sqrtf(cos_t2)));
+    r->origin = position;
+    r->tmax = 5000.0f;
+    r->tmin = ETA;
+    h->has_hit = 0;
+    return add(ph, V(0, 0, 0));
+}
+
+static void sample_w6e3(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, float out[3], uint32_t* prim)
+{
+    /* fs_main, w6e3.wgsl:166-192 */
+    const or_uniform* u = C->u;
+    uint32_t subdiv = u->subdivision_level;
+    v3 result = V(0, 0, 0);
+    float ux, uy;
+    pixel_uv(u, x, y, &ux, &uy);
+    *prim = 0xFFFFFFFFu;
+    for (uint32_t sample = 0; sample < subdiv * subdiv; sample++) {
+        float jx = C->jitter ? C->jitter[2 * sample] : 0.0f;
+        float jy = C->jitter ? C->jitter[2 * sample + 1] : 0.0f;
+        Ray r;
+        r.direction = cam_dir(cam, ux, uy, jx, jy);
+        r.origin = cam->e;
+        r.tmax = 5000.0f;
+        r.tmin = 0.001f;
+        Hit h;
+        memset(&h, 0, sizeof h);
+        C->c.primary++;
+        for (int i = 0; i < 10; i++) {
+            if (i > 0) C->c.bounce++;
+            if (intersect_scene_w6e3(C, &r, &h)) {
+                if (i == 0 && sample + 1 == subdiv * subdiv && h.shader == 0) *prim = h.tri;
+                result = add(result, shade_w6e3(C, &r, &h));
+            } else {
+                result = add(result, V(0.0f, 0.0f, 0.0f));
+                break;
+            }
+            if (h.has_hit) break;
+        }
+    }
+    result = muls(result, 1.0f / (float)(subdiv * subdiv));
+    out[0] = result.x;
+    out[1] = result.y;
+    out[2] = result.z;
 }
 
 /* ------------------------------------------------------------ W1E6 */
@@ -1219,7 +1350,8 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
         size_t o = (size_t)ry * J->w + rx;
         float* acc = J->accum + 4 * o;
         uint32_t prim = 0xFFFFFFFFu;
-        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 || (J->mode >= OR_MODE_W8E1 && J->mode != OR_MODE_W6E2)) {
+        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 ||
+            (J->mode >= OR_MODE_W8E1 && J->mode != OR_MODE_W6E2 && J->mode != OR_MODE_W6E3)) {
             /* progressive */
             const int clamp0 = J->mode != OR_MODE_W7E1 && J->mode != OR_MODE_W7E2;   /* w7e1.wgsl:229-235: no max */
             float a[3] = {acc[0], acc[1], acc[2]};
@@ -1244,6 +1376,7 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
             C->c.samples++;
             if (J->mode == OR_MODE_W1E6) sample_w1e6(C, cam, x, y, res, &prim);
             else if (J->mode == OR_MODE_W6E2) sample_w6e2(C, cam, x, y, res, &prim);
+            else if (J->mode == OR_MODE_W6E3) sample_w6e3(C, cam, x, y, res, &prim);
             else sample_w6e1(C, cam, x, y, res, &prim);
             acc[0] = res[0]; acc[1] = res[1]; acc[2] = res[2]; acc[3] = 1.0f;
         }
@@ -1279,7 +1412,7 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
               uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
               float* accum, uint32_t* ids, or_counts* counts, int nthreads)
 {
-    if (mode < 0 || mode > OR_MODE_W7E2) return -1;
+    if (mode < 0 || mode > OR_MODE_W6E3) return -1;
     if (mode != OR_MODE_W1E6) {
         if (!s || !s->nmats) return -1;
         if (trav == OR_TRAV_BSP && (!s->tree || !s->planes)) return -1;

@@ -58,3 +58,26 @@ def test_scene_through_render_state(rt, name):
         assert rs.iteration == (2 if rs.mode != "W6E2" else 0)
     finally:
         rs.ctx.close()
+
+
+@pytest.fixture(scope="module", params=["BSP", "BVH"])
+def balls(request, rt, gpu):
+    return Scene(rt, rt.Mesh.from_obj(model("CornellBox.obj")), request.param)
+
+
+def test_w6e3_mirror_and_glossy_balls(balls):
+    # w6e3.wgsl: the mirror ball, the glossy ball (Phong lobe with the pinned
+    # pow(., 42) + refraction, magenta under total internal reflection), the box
+    g = balls.render_gpu("W6E3", CORNELL_CAM, 128, 128, (0, 0, 128, 128), 0, 1)
+    o = balls.render_oracle("W6E3", CORNELL_CAM, 128, 128, (0, 0, 128, 128), 0, 1)
+    check(g, o)
+    assert g[2]["bounce"] > 0 and (g[1] == 0xFFFFFFFF).sum() > 100
+
+
+def test_w6e3_subdivision_region(rt, balls):
+    J = __import__("importlib").import_module("02562_raytracer_amd.jitter")
+    jit = J.jitters_for(512, 2)
+    region = (120, 290, 300, 150)   # both balls at the scene's 512x512
+    g = balls.render_gpu("W6E3", CORNELL_CAM, 512, 512, region, 0, 1, jitter=jit)
+    o = balls.render_oracle("W6E3", CORNELL_CAM, 512, 512, region, 0, 1, jitter=jit)
+    check(g, o)
