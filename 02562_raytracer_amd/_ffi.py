@@ -23,7 +23,7 @@ RT_E_IO = -5
 RT_E_UNSUPPORTED = -6
 
 (RT_MODE_W1E6, RT_MODE_W6E1, RT_MODE_PROJECT, RT_MODE_W7E3, RT_MODE_W9E1, RT_MODE_W8E1, RT_MODE_W8E2, RT_MODE_W8E3,
- RT_MODE_W9E2, RT_MODE_W6E2, RT_MODE_W7E1, RT_MODE_W7E2, RT_MODE_W6E3) = range(13)
+ RT_MODE_W9E2, RT_MODE_W6E2, RT_MODE_W7E1, RT_MODE_W7E2, RT_MODE_W6E3, RT_MODE_W9E3) = range(14)
 RT_TRAVERSE_BSP, RT_TRAVERSE_BVH, RT_TRAVERSE_NONE = range(3)
 RT_OPT_DETAIL_COUNTERS = 1
 RT_OPT_WAVES_PER_CU = 2
@@ -37,9 +37,9 @@ RT_OPT_MIN_HALF_LANES = 8
 MODES = {"W1E6": RT_MODE_W1E6, "W6E1": RT_MODE_W6E1, "PROJECT": RT_MODE_PROJECT, "W7E3": RT_MODE_W7E3,
          "W9E1": RT_MODE_W9E1, "W8E1": RT_MODE_W8E1, "W8E2": RT_MODE_W8E2, "W8E3": RT_MODE_W8E3,
          "W9E2": RT_MODE_W9E2, "W6E2": RT_MODE_W6E2, "W7E1": RT_MODE_W7E1, "W7E2": RT_MODE_W7E2,
-         "W6E3": RT_MODE_W6E3}
+         "W6E3": RT_MODE_W6E3, "W9E3": RT_MODE_W9E3}
 # progressive path tracers (per-iteration samples folded in order)
-PATH_MODES = ("W7E3", "W9E1", "W8E1", "W8E2", "W8E3", "W9E2", "W7E1", "W7E2")
+PATH_MODES = ("W7E3", "W9E1", "W8E1", "W8E2", "W8E3", "W9E2", "W7E1", "W7E2", "W9E3")
 TRAVERSALS = {"BSP": RT_TRAVERSE_BSP, "BVH": RT_TRAVERSE_BVH, "NONE": RT_TRAVERSE_NONE}
 
 u32p = C.POINTER(C.c_uint32)

@@ -778,12 +778,12 @@ int rt_set_environment_map(rt_ctx* c, const uint8_t* rgba8, uint32_t width, uint
 static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
 {
     if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
-    if (mode < RT_MODE_W1E6 || mode > RT_MODE_W6E3) return fail(c, RT_E_INVALID, "rt_render: bad mode");
+    if (mode < RT_MODE_W1E6 || mode > RT_MODE_W9E3) return fail(c, RT_E_INVALID, "rt_render: bad mode");
     // W7E1/W7E2: progressive, folded inside k_direct (no per-iteration samples)
     const bool direct_prog = mode == RT_MODE_W7E1 || mode == RT_MODE_W7E2;
     // progressive path tracers: per-iteration samples, folded in order by k_fold
     const bool path = mode == RT_MODE_W7E3 || mode == RT_MODE_W9E1 || mode == RT_MODE_W8E1 || mode == RT_MODE_W8E2 ||
-                      mode == RT_MODE_W8E3 || mode == RT_MODE_W9E2;
+                      mode == RT_MODE_W8E3 || mode == RT_MODE_W9E2 || mode == RT_MODE_W9E3;
     if (mode == RT_MODE_W1E6) {
         if (trav != RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "W1E6 is analytic: traverse must be NONE");
     } else {
@@ -791,7 +791,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
         if (trav == RT_TRAVERSE_BSP && !c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_render: no BSP uploaded");
         if (trav == RT_TRAVERSE_BVH && !c->has_bvh) return fail(c, RT_E_NOT_READY, "rt_render: no BVH uploaded");
         if (trav == RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "mesh modes need BSP or BVH");
-        if (path && mode != RT_MODE_W9E1 && mode != RT_MODE_W9E2 && c->nlights < 2)
+        if (path && mode != RT_MODE_W9E1 && mode != RT_MODE_W9E2 && mode != RT_MODE_W9E3 && c->nlights < 2)
             return fail(c, RT_E_INVALID, "W7E3/W8 sample area lights: the mesh has no emissive (illum 1) triangle");
         if ((mode == RT_MODE_W6E1 || mode == RT_MODE_PROJECT) && trav == RT_TRAVERSE_BSP && !c->has_bsp)
             return fail(c, RT_E_NOT_READY, "rt_render: W6E1/PROJECT need the BSP root AABB");

@@ -193,7 +193,9 @@ __device__ __forceinline__ void pixel_uv(const rt_uniform& u, uint32_t x, uint32
 // caller resolves the bound exactly).  exact_bounds: tmin and tmax are the
 // shader's values (the BSP walk keeps approximate pushed t values, see
 // bsp_decide).
-template <bool FAST, bool COUNT = false>
+// CULL: the back-face culling test of w9e3.wgsl:328 (|denom| < 5e-5 or
+// denom > 0 rejects) in place of |denom| < 1e-10.
+template <bool FAST, bool COUNT = false, bool CULL = false>
 __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const float4 r2, f3 o, f3 w, float tmin,
                                          float tmax, float& dist, float& beta, float& gamma, Counters* cn = nullptr)
 {
@@ -205,7 +207,7 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
     const float a = dot(nom, e1);
     const float b = -dot(nom, e0);
     const float c = dot(ov, n);
-    bool reject = rt_absf(denom) < 1e-10f;
+    bool reject = CULL ? ((rt_absf(denom) < 0.00005f) | (denom > 0.0f)) : rt_absf(denom) < 1e-10f;
     if (FAST) {
         // certain rejections, each implying the exact predicate below rejects:
         // a sign (beta < 0 / gamma < 0), the distance range, or
@@ -344,7 +346,7 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 // A walk that reaches a leaf starts its triangle range (tested from the next
 // trip on); an empty leaf, or a leaf tested without a hit, pops.  Leaf ranges
 // (leaf_k, leaf_end, hit_k) are byte offsets of records in that buffer.
-template <bool COUNT>
+template <bool COUNT, bool CULL = false>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
 {
@@ -373,7 +375,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             c.v[C_TESTS]++;
         }
         float dist, beta, gamma;
-        if (tri_math<true, COUNT>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+        if (tri_math<true, COUNT, CULL>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
@@ -494,7 +496,7 @@ __device__ __forceinline__ void bvh_init(Trav& t, float tmin, float tmax)
 // {min.xyz, w0}{max.xyz, w1}, interior w0 = byte offset of the right child
 // (the left child is the next record), w1 = 0; leaf w0 = byte offset of its
 // first triangle record, w1 = 48 * n_prims.
-template <bool COUNT>
+template <bool COUNT, bool CULL = false>
 __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const BvhDeep& dp, const f3 o, const f3 d,
                                          const f3 inv, bool anyhit, Trav& t, Counters& c)
 {
@@ -513,7 +515,7 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
         }
         float dist, beta, gamma;
         // the BVH walk never narrows the ray interval: both bounds are exact
-        if (tri_math<true, COUNT>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+        if (tri_math<true, COUNT, CULL>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
@@ -562,13 +564,13 @@ __device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float
     if (TRAV == RT_TRAVERSE_BVH) bvh_init(t, tmin, tmax);
     else trav_init(t, tmin, tmax);
 }
-template <int TRAV, bool COUNT>
+template <int TRAV, bool COUNT, bool CULL = false>
 __device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const BvhDeep& dp, const f3 o, const f3 d,
                                           const f3 inv, bool anyhit, Trav& t, Counters& c)
 {
     if (TRAV == RT_TRAVERSE_BVH)
-        return bvh_step<COUNT>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv, anyhit, t, c);
-    return bsp_step<COUNT>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
+        return bvh_step<COUNT, CULL>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv, anyhit, t, c);
+    return bsp_step<COUNT, CULL>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
 }
 
 // Whole traversal of one ray (used by the primary-ray kernel).
@@ -591,7 +593,8 @@ struct HitRec {
     uint32_t tri, material;
     f3 pos, nrm;
 };
-template <int TRAV>
+// ETA_W: w9e3.wgsl:343 adds ETA (1e-4) to each interpolation weight
+template <int TRAV, bool ETA_W = false>
 __device__ __forceinline__ HitRec resolve(const DevScene& S, const TraceOut& t, const f3 o, const f3 d,
                                           bool face_normals)
 {
@@ -612,7 +615,11 @@ __device__ __forceinline__ HitRec resolve(const DevScene& S, const TraceOut& t, 
         n1 = ld3(S.nrm[ix.y]);
         n2 = ld3(S.nrm[ix.z]);
     }
-    h.nrm = normalize(add(add(muls(n0, 1.0f - t.beta - t.gamma), muls(n1, t.beta)), muls(n2, t.gamma)));
+    if (ETA_W)
+        h.nrm = normalize(add(add(muls(n0, 1.0f - t.beta - t.gamma + 0.0001f), muls(n1, t.beta + 0.0001f)),
+                              muls(n2, t.gamma + 0.0001f)));
+    else
+        h.nrm = normalize(add(add(muls(n0, 1.0f - t.beta - t.gamma), muls(n1, t.beta)), muls(n2, t.gamma)));
     h.material = ix.w;
     return h;
 }
@@ -764,6 +771,16 @@ __device__ __forceinline__ bool w9_plane(f3 o, f3 w, float tmin, float& tmax)
     return true;
 }
 
+// sample_directional_light (w9e3.wgsl:405-414): the sun, L = 10, from -normalize(1, -0.35, 0)
+__device__ __forceinline__ Light sun_light()
+{
+    Light L;
+    L.l_i = V(10.0f, 10.0f, 10.0f);
+    L.w_i = neg(normalize(V(1.0f, -0.35f, 0.0f)));
+    L.dist = 999999.0f;
+    return L;
+}
+
 // tmax of a closest-hit ray [ETA, 5000] from o along w: the analytic objects
 // the shader tests before intersect_trimesh bound the mesh walk (r.tmax)
 template <int MODE>
@@ -771,7 +788,7 @@ __device__ __forceinline__ float ray_tmax(f3 o, f3 w, float eta)
 {
     float tm = 5000.0f;
     if (MODE == RT_MODE_W8E1 || MODE == RT_MODE_W8E2 || MODE == RT_MODE_W8E3) tm = w8_balls(o, w, eta, 5000.0f).t;
-    if (MODE == RT_MODE_W9E2) w9_plane(o, w, eta, tm);
+    if (MODE == RT_MODE_W9E2 || MODE == RT_MODE_W9E3) w9_plane(o, w, eta, tm);
     return tm;
 }
 
@@ -886,8 +903,13 @@ k_path(DevScene S, DevLaunch L)
     // W9E2: W9E1 + the holdout plane y = 0 (ambient-occlusion ray, environment
     // seen through it) and an RGBE environment; one instantiation for all its shaders
     constexpr bool W9E2 = MODE == RT_MODE_W9E2;
-    constexpr bool W9 = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT || W9E2;
-    constexpr bool XT = MODE == MODE_W9E1_TRANSPARENT || W9E2;
+    // W9E3: the holdout plane shaded by an ambient-occlusion ray and a sun ray,
+    // a sun-lit lambertian, back-face culled triangles, transparent at selection 3
+    constexpr bool W9E3 = MODE == RT_MODE_W9E3;
+    constexpr bool PLANE = W9E2 || W9E3;
+    constexpr bool W9 = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT || W9E2 || W9E3;
+    constexpr bool XT = MODE == MODE_W9E1_TRANSPARENT || W9E2 || W9E3;
+    constexpr uint32_t TSEL = W9E3 ? 3u : 7u;   // the transparent shader's selection value
     // W8E1/W8E2/W8E3: the Cornell box with its two analytic balls; W8E1 lights
     // directly only (10 segments), W8E2/W8E3 path trace with a firefly clamp
     constexpr bool W8 = MODE == RT_MODE_W8E1 || MODE == RT_MODE_W8E2 || MODE == RT_MODE_W8E3;
@@ -916,7 +938,8 @@ k_path(DevScene S, DevLaunch L)
     // lane state: ST_IDLE (no pixel), ST_TRACE (a ray in flight), ST_SHADE (ray done, waiting to shade)
     enum : uint32_t { ST_IDLE = 0, ST_TRACE = 1, ST_SHADE = 2 };
     uint32_t st = ST_IDLE;
-    bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false, ao = false;
+    bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false, ao = false, hblk = false;
+    uint32_t hph = 0;   // W9E3 holdout: 1 = occlusion ray in flight, 2 = sun ray in flight
     uint32_t px = 0, py = 0, out = 0, it = 0, unit_end = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
     f3 res = V(0, 0, 0), fac = V(1, 1, 1), ro = V(0, 0, 0), rd = V(0, 0, 1), inv = V(0, 0, 0);
     f3 ndir = V(0, 0, 1), cu = V(0, 0, 0), cb = V(0, 0, 0);
@@ -945,6 +968,7 @@ k_path(DevScene S, DevLaunch L)
         trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
         st = ST_TRACE;
         ao = false;
+        hph = 0;
         cnt.v[C_SAMPLES]++;
         cnt.v[C_PRIMARY]++;
     };
@@ -983,7 +1007,7 @@ k_path(DevScene S, DevLaunch L)
                 go = go && (leafst ? (nl >= KH || nn < KH) : (nn >= KH || nl < KH));
             }
             if (go) {
-                if (trav_step<TRAV, COUNT>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                if (trav_step<TRAV, COUNT, W9E3>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }
         }
         if (COUNT) {
@@ -1000,7 +1024,7 @@ k_path(DevScene S, DevLaunch L)
             bool sample_done = false;
             if (!shadow) {
                 if (tr.found) {
-                    const HitRec h = resolve<TRAV>(S, trav_out(tr), ro, rd, !W9);
+                    const HitRec h = resolve<TRAV, W9E3>(S, trav_out(tr), ro, rd, !W9);
                     if (bounce == 0) prim = h.tri;
                     const rt_material& m = mat_of(S, h.material);
                     if (sel == 0u) {
@@ -1008,7 +1032,9 @@ k_path(DevScene S, DevLaunch L)
                         const f3 brdf = divs(ld3(m.diffuse), RT_PI_F);
                         const f3 emission = ld3(m.ambient);
                         Light Lt;
-                        if (W9) {
+                        if (W9E3) {
+                            Lt = sun_light();   // sample_directional_light, w9e3.wgsl:405-414
+                        } else if (W9) {
                             Lt.l_i = V(0, 0, 0);   // light_init(), w9e1.wgsl:67-73
                             Lt.w_i = V(0.0f, 1.0f, 0.0f);
                             Lt.dist = 999999.0f;
@@ -1042,16 +1068,16 @@ k_path(DevScene S, DevLaunch L)
                         cnt.v[C_SHADOW]++;
                         float tpl = Lt.dist - ETA;
                         if ((W8 && w8_balls(ro, rd, ETA, Lt.dist - ETA).id != 0u) ||
-                            (W9E2 && w9_plane(ro, rd, ETA, tpl))) {
+                            (PLANE && w9_plane(ro, rd, ETA, tpl))) {
                             tr.found = true;   // a ball / the plane blocks the light: no mesh walk
                             st = ST_SHADE;
                         } else {
                             trav_start<TRAV>(tr, stk, ETA, Lt.dist - ETA);
                         }
-                    } else if (sel == 2u || (XT && sel == 7u)) {
+                    } else if (sel == 2u || (XT && sel == TSEL)) {
                         f3 n = h.nrm;
                         bool reflect_ray = true;
-                        if (XT && sel == 7u) {
+                        if (XT && sel == TSEL) {
                             // transparent (w9e1.wgsl:505-558); hit_record_init: ior1_over_ior2 1.0,
                             // extinction (1,1,1).  The refracted ray replaces r before the mirror
                             // branch reflects it (as the shader does).
@@ -1059,7 +1085,8 @@ k_path(DevScene S, DevLaunch L)
                             const f3 normal = normalize(h.nrm);
                             const f3 ext = V(1.0f, 1.0f, 1.0f);
                             f3 out_n;
-                            float ior = 1.0f, cos_i = dot(w_i, normal), absorption = 0.0f;
+                            // W9E3's intersect_scene_bsp sets ior1_over_ior2 = 1.5 on mesh hits
+                            float ior = W9E3 ? 1.5f : 1.0f, cos_i = dot(w_i, normal), absorption = 0.0f;
                             if (cos_i < 0.0f) {
                                 cos_i = dot(w_i, neg(normal));
                                 out_n = neg(normal);
@@ -1129,7 +1156,26 @@ k_path(DevScene S, DevLaunch L)
                         }
                     } else {
                         float tpl = 5000.0f;
-                        if (W9E2 && w9_plane(ro, rd, ETA, tpl)) {
+                        if (W9E3 && w9_plane(ro, rd, ETA, tpl)) {
+                            // holdout_shader (w9e3.wgsl:490-517): environment * factor, less 0.5
+                            // for an occluded cosine ray and 0.5 for a blocked sun ray; both
+                            // through intersect_scene_bsp (plane + mesh)
+                            cu = mul(env_at<MODE>(L, env, rd), fac);
+                            ro = add(ro, muls(rd, tpl));   // ray_at
+                            rd = indirect_dir(V(0.0f, 1.0f, 0.0f), rng);
+                            inv = trav_inv<TRAV>(rd);
+                            shadow = true;
+                            hph = 1;
+                            st = ST_TRACE;
+                            cnt.v[C_SHADOW]++;
+                            float tp2 = 5000.0f;
+                            if (w9_plane(ro, rd, ETA, tp2)) {
+                                tr.found = true;
+                                st = ST_SHADE;
+                            } else {
+                                trav_start<TRAV>(tr, stk, ETA, 5000.0f);
+                            }
+                        } else if (W9E2 && w9_plane(ro, rd, ETA, tpl)) {
                             // holdout_shader (w9e2.wgsl:514-537): an any-hit ambient-occlusion
                             // ray about the plane normal; unoccluded, the environment behind
                             ndir = rd;
@@ -1148,6 +1194,27 @@ k_path(DevScene S, DevLaunch L)
                         }
                     }
                 }
+            } else if (W9E3 && hph == 1u) {
+                // occlusion ray finished: the sun ray from the same plane point
+                hblk = tr.found;
+                rd = sun_light().w_i;
+                inv = trav_inv<TRAV>(rd);
+                hph = 2;
+                st = ST_TRACE;
+                cnt.v[C_SHADOW]++;
+                float tp2 = 5000.0f;
+                if (w9_plane(ro, rd, ETA, tp2)) {
+                    tr.found = true;
+                    st = ST_SHADE;
+                } else {
+                    trav_start<TRAV>(tr, stk, ETA, 5000.0f);
+                }
+            } else if (W9E3 && hph == 2u) {
+                float contribution = 1.0f;
+                if (hblk) contribution -= 0.5f;
+                if (tr.found) contribution -= 0.5f;
+                res = add(res, muls(cu, contribution));
+                sample_done = true;
             } else if (W9E2 && ao) {
                 // ambient-occlusion ray finished: occluded adds vec3(0); the sample ends
                 res = add(res, tr.found ? V(0, 0, 0) : mul(env_at<MODE>(L, env, ndir), fac));
@@ -1919,6 +1986,12 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
             else detail ? launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
                         : launch_path<RT_MODE_W9E1, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         }
+        break;
+    case RT_MODE_W9E3:
+        if (bvh) detail ? launch_path<RT_MODE_W9E3, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)
+                        : launch_path<RT_MODE_W9E3, RT_TRAVERSE_BVH, false>(s, l, grid, lds, stream);
+        else detail ? launch_path<RT_MODE_W9E3, RT_TRAVERSE_BSP, true>(s, l, grid, lds, stream)
+                    : launch_path<RT_MODE_W9E3, RT_TRAVERSE_BSP, false>(s, l, grid, lds, stream);
         break;
     case RT_MODE_W9E2:
         if (bvh) detail ? launch_path<RT_MODE_W9E2, RT_TRAVERSE_BVH, true>(s, l, grid, lds, stream)

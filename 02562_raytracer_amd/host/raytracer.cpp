@@ -111,6 +111,7 @@ std::optional<rt_mode> SceneDescriptor::mode() const
     if (shader == "w7e1.wgsl") return RT_MODE_W7E1;
     if (shader == "w7e2.wgsl") return RT_MODE_W7E2;
     if (shader == "w6e3.wgsl") return RT_MODE_W6E3;
+    if (shader == "w9e3.wgsl") return RT_MODE_W9E3;
     return std::nullopt;
 }
 
@@ -389,7 +390,7 @@ void RenderState::render(uint32_t spp)
                "render");
     const bool path = mode_ == RT_MODE_W7E3 || mode_ == RT_MODE_W9E1 || mode_ == RT_MODE_W8E1 ||
                       mode_ == RT_MODE_W8E2 || mode_ == RT_MODE_W8E3 || mode_ == RT_MODE_W9E2 ||
-                      mode_ == RT_MODE_W7E1 || mode_ == RT_MODE_W7E2;
+                      mode_ == RT_MODE_W7E1 || mode_ == RT_MODE_W7E2 || mode_ == RT_MODE_W9E3;
     if (progressive_ && path) iteration_ += spp;
     update();
 }

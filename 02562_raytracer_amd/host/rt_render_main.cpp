@@ -68,6 +68,7 @@ static const char* mode_name(std::optional<rt_mode> m)
     case RT_MODE_W7E1: return "W7E1";
     case RT_MODE_W7E2: return "W7E2";
     case RT_MODE_W6E3: return "W6E3";
+    case RT_MODE_W9E3: return "W9E3";
     }
     return nullptr;
 }

@@ -23,6 +23,7 @@ SHADER_MODES = {
     "w7e1.wgsl": "W7E1",
     "w7e2.wgsl": "W7E2",
     "w6e3.wgsl": "W6E3",
+    "w9e3.wgsl": "W9E3",
 }
 
 

@@ -98,7 +98,8 @@ typedef enum rt_mode {
     RT_MODE_W6E2    = 9,  /* res/shaders/w6e2.wgsl: direct light from every area-light centre, subdiv^2 samples */
     RT_MODE_W7E1    = 10, /* res/shaders/w7e1.wgsl: as W6E2, progressive (TEA jitter), no max(., 0) */
     RT_MODE_W7E2    = 11, /* res/shaders/w7e2.wgsl: random area-light points, progressive */
-    RT_MODE_W6E3    = 12  /* res/shaders/w6e3.wgsl: W6E2's box + mirror ball and glossy (Phong + refraction) ball */
+    RT_MODE_W6E3    = 12, /* res/shaders/w6e3.wgsl: W6E2's box + mirror ball and glossy (Phong + refraction) ball */
+    RT_MODE_W9E3    = 13  /* res/shaders/w9e3.wgsl: sun light, holdout plane (AO + sun rays), culled triangles */
 } rt_mode;
 
 /* SceneDescriptor.traverse_type, src/scenes.rs:13-17 */

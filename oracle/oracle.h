@@ -81,7 +81,7 @@ typedef struct or_counts {
 
 enum { OR_MODE_W1E6 = 0, OR_MODE_W6E1 = 1, OR_MODE_PROJECT = 2, OR_MODE_W7E3 = 3, OR_MODE_W9E1 = 4,
        OR_MODE_W8E1 = 5, OR_MODE_W8E2 = 6, OR_MODE_W8E3 = 7, OR_MODE_W9E2 = 8,
-       OR_MODE_W6E2 = 9, OR_MODE_W7E1 = 10, OR_MODE_W7E2 = 11, OR_MODE_W6E3 = 12 };
+       OR_MODE_W6E2 = 9, OR_MODE_W7E1 = 10, OR_MODE_W7E2 = 11, OR_MODE_W6E3 = 12, OR_MODE_W9E3 = 13 };
 enum { OR_TRAV_BSP = 0, OR_TRAV_BVH = 1, OR_TRAV_NONE = 2 };
 
 /* ---- mesh ---- */

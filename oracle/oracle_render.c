@@ -96,7 +96,11 @@ static int tri_test(Ctx* C, Ray* r, Hit* h, uint32_t v, int face_normals)
     v3 normal = cross(e0, e1);
     v3 nom = cross(o_to_v0, w_i);
     float denom = dot(w_i, normal);
-    if (rt_absf(denom) < 1e-10f) return 0;
+    if (C->mode == OR_MODE_W9E3) {   /* w9e3.wgsl:328: back faces and grazing hits rejected */
+        if (rt_absf(denom) < 0.00005f || denom > 0.0f) return 0;
+    } else if (rt_absf(denom) < 1e-10f) {
+        return 0;
+    }
     float beta = dot(nom, e1) / denom;
     float gamma = -dot(nom, e0) / denom;
     float distance = dot(o_to_v0, normal) / denom;
@@ -114,7 +118,11 @@ static int tri_test(Ctx* C, Ray* r, Hit* h, uint32_t v, int face_normals)
     r->tmax = distance;
     h->dist = distance;
     h->position = add(o, muls(w_i, distance));   /* ray_at */
-    h->normal = normalize(add(add(muls(n0, 1.0f - beta - gamma), muls(n1, beta)), muls(n2, gamma)));
+    if (C->mode == OR_MODE_W9E3)   /* w9e3.wgsl:343: ETA (1e-4) on every weight */
+        h->normal = normalize(add(add(muls(n0, 1.0f - beta - gamma + 0.0001f), muls(n1, beta + 0.0001f)),
+                                  muls(n2, gamma + 0.0001f)));
+    else
+        h->normal = normalize(add(add(muls(n0, 1.0f - beta - gamma), muls(n1, beta)), muls(n2, gamma)));
     h->material = ix[3];
     h->tri = v;
     return 1;
@@ -453,6 +461,48 @@ static v3 holdout_w9e2(Ctx* C, Ray* r, Hit* h, uint32_t* t)   /* holdout_shader,
     return mul(env_lookup(C, r->direction), h->factor);
 }
 
+static Light sun_light_w9e3(void)   /* sample_directional_light, w9e3.wgsl:405-414 */
+{
+    Light L;
+    L.l_i = V(10.0f, 10.0f, 10.0f);
+    L.w_i = neg(normalize(V(1.0f, -0.35f, 0.0f)));
+    L.dist = 999999.0f;
+    return L;
+}
+
+static v3 holdout_w9e3(Ctx* C, Ray* r, Hit* h, uint32_t* t)   /* holdout_shader, w9e3.wgsl:490-517 */
+{
+    const float ETA = 0.0001f;
+    float contribution = 1.0f;
+    v3 normal = normalize(h->normal);
+    float xi1 = rnd(t);
+    float xi2 = rnd(t);
+    float thet = rt_det_acosf(rt_det_sqrtf(1.0f - xi1));
+    float phi = 2.0f * PI_F * xi2;
+    float st = rt_det_sinf(thet), ct = rt_det_cosf(thet);
+    v3 tang = V(st * rt_det_cosf(phi), st * rt_det_sinf(phi), ct);
+    v3 direct_dir = rotate_to_normal(normal, tang);
+    v3 color = mul(env_lookup(C, r->direction), h->factor);
+    Hit hi;
+    memset(&hi, 0, sizeof hi);
+    Ray ray;
+    ray.direction = direct_dir;   /* ray_init */
+    ray.origin = h->position;
+    ray.tmax = 5000.0f;
+    ray.tmin = ETA;
+    C->c.shadow++;
+    if (intersect_scene_w9e2(C, &ray, &hi)) contribution -= 0.5f;
+    Light L = sun_light_w9e3();
+    ray.direction = L.w_i;
+    ray.origin = h->position;
+    ray.tmax = 5000.0f;
+    ray.tmin = ETA;
+    C->c.shadow++;
+    if (intersect_scene_w9e2(C, &ray, &hi)) contribution -= 0.5f;
+    h->has_hit = 1;
+    return muls(color, contribution);
+}
+
 static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
 {
     /* shade (w9e1.wgsl) with selection1; lambertian with light_init() (:428-470) */
@@ -460,8 +510,11 @@ static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
     const float ETA = 0.0001f;
     h->has_hit = 1;
     if (C->mode == OR_MODE_W9E2 && h->shader == SH_HOLDOUT) return holdout_w9e2(C, r, h, t);
+    if (C->mode == OR_MODE_W9E3 && h->shader == SH_HOLDOUT) return holdout_w9e3(C, r, h, t);
     const or_material* m = mat_of(s, h->material);
-    switch (C->u->selection1) {
+    uint32_t selc = C->u->selection1;
+    if (C->mode == OR_MODE_W9E3) selc = selc == 3u ? 7u : (selc == 7u ? 0xFFu : selc);   /* transparent is case 3 */
+    switch (selc) {
     case 0: {
         v3 brdf = divs(load3(m->diffuse), PI_F);
         v3 emission = load3(m->ambient);
@@ -471,6 +524,7 @@ static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
         L.l_i = V(0, 0, 0);
         L.w_i = V(0.0f, 1.0f, 0.0f);
         L.dist = 999999.0f;
+        if (C->mode == OR_MODE_W9E3) L = sun_light_w9e3();
         Ray sr;
         sr.direction = L.w_i;
         sr.origin = h->position;
@@ -479,7 +533,8 @@ static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
         Hit hi;
         memset(&hi, 0, sizeof hi);
         C->c.shadow++;
-        int blocked = C->mode == OR_MODE_W9E2 ? intersect_scene_w9e2(C, &sr, &hi) : trace(C, &sr, &hi, 0);
+        int blocked = (C->mode == OR_MODE_W9E2 || C->mode == OR_MODE_W9E3) ? intersect_scene_w9e2(C, &sr, &hi)
+                                                                          : trace(C, &sr, &hi, 0);
         if (!blocked) diffuse = mul(muls(brdf, rt_satf(dot(normal, L.w_i))), L.l_i);
         if (h->emit) ambient = mul(emission, h->factor);
         diffuse = mul(diffuse, h->factor);
@@ -511,7 +566,7 @@ static v3 shade_w9e1(Ctx* C, Ray* r, Hit* h, uint32_t* t)
         v3 w_i = neg(normalize(r->direction));
         v3 normal = normalize(h->normal);
         v3 out_normal;
-        float ior = 1.0f;
+        float ior = C->mode == OR_MODE_W9E3 ? 1.5f : 1.0f;   /* W9E3 sets ior1_over_ior2 = 1.5 on mesh hits */
         float cos_i = dot(w_i, normal);
         float absorption = 0.0f;
         v3 extinction = V(1.0f, 1.0f, 1.0f);
@@ -785,7 +840,8 @@ static void sample_path(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t
                         uint32_t* prim)
 {
     const or_uniform* u = C->u;
-    int w9 = C->mode == OR_MODE_W9E1 || C->mode == OR_MODE_W9E2;
+    int w9 = C->mode == OR_MODE_W9E1 || C->mode == OR_MODE_W9E2 || C->mode == OR_MODE_W9E3;
+    int plane = C->mode == OR_MODE_W9E2 || C->mode == OR_MODE_W9E3;
     float eta = w9 ? 0.0001f : 0.01f;
     uint32_t launch_idx = y * u->resolution[0] + x;
     uint32_t t = tea16(launch_idx, it);
@@ -809,9 +865,9 @@ static void sample_path(Ctx* C, const Cam* cam, uint32_t x, uint32_t y, uint32_t
     C->c.primary++;
     for (int i = 0; i < 50; i++) {
         if (i > 0) C->c.bounce++;
-        int hit = C->mode == OR_MODE_W9E2 ? intersect_scene_w9e2(C, &r, &h) : trace(C, &r, &h, !w9);
+        int hit = plane ? intersect_scene_w9e2(C, &r, &h) : trace(C, &r, &h, !w9);
         if (hit) {
-            if (i == 0 && !(C->mode == OR_MODE_W9E2 && h.shader == SH_HOLDOUT)) *prim = h.tri;
+            if (i == 0 && !(plane && h.shader == SH_HOLDOUT)) *prim = h.tri;
             result = add(result, w9 ? shade_w9e1(C, &r, &h, &t) : shade_w7e3(C, &r, &h, &t));
         } else {
             if (w9)   /* environment_map(r.direction) * hit.factor, w9e1.wgsl:264-265 */
@@ -1350,7 +1406,7 @@ static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
         size_t o = (size_t)ry * J->w + rx;
         float* acc = J->accum + 4 * o;
         uint32_t prim = 0xFFFFFFFFu;
-        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 ||
+        if (J->mode == OR_MODE_W7E3 || J->mode == OR_MODE_W9E1 || J->mode == OR_MODE_W9E3 ||
             (J->mode >= OR_MODE_W8E1 && J->mode != OR_MODE_W6E2 && J->mode != OR_MODE_W6E3)) {
             /* progressive */
             const int clamp0 = J->mode != OR_MODE_W7E1 && J->mode != OR_MODE_W7E2;   /* w7e1.wgsl:229-235: no max */
@@ -1412,7 +1468,7 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
               uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
               float* accum, uint32_t* ids, or_counts* counts, int nthreads)
 {
-    if (mode < 0 || mode > OR_MODE_W6E3) return -1;
+    if (mode < 0 || mode > OR_MODE_W9E3) return -1;
     if (mode != OR_MODE_W1E6) {
         if (!s || !s->nmats) return -1;
         if (trav == OR_TRAV_BSP && (!s->tree || !s->planes)) return -1;

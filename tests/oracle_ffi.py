@@ -72,7 +72,7 @@ class Bvh(C.Structure):
                 ("nids", C.c_uint32)]
 
 
-MODES = {"W1E6": 0, "W6E1": 1, "PROJECT": 2, "W7E3": 3, "W9E1": 4, "W8E1": 5, "W8E2": 6, "W8E3": 7, "W9E2": 8, "W6E2": 9, "W7E1": 10, "W7E2": 11, "W6E3": 12}
+MODES = {"W1E6": 0, "W6E1": 1, "PROJECT": 2, "W7E3": 3, "W9E1": 4, "W8E1": 5, "W8E2": 6, "W8E3": 7, "W9E2": 8, "W6E2": 9, "W7E1": 10, "W7E2": 11, "W6E3": 12, "W9E3": 13}
 TRAVS = {"BSP": 0, "BVH": 1, "NONE": 2}
 
 _lib = None

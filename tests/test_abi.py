@@ -63,7 +63,7 @@ def test_scene_table_mirrors_reference(rt):
     assert names[0] == "W1 E1" and names[-1] == "Project: Dragon BSP"
     hot = [s for s in sc if s.mode]
     assert {s.mode for s in hot} == {"W1E6", "W6E1", "PROJECT", "W7E3", "W9E1", "W8E1", "W8E2", "W8E3", "W9E2", "W6E2",
-                                      "W7E1", "W7E2", "W6E3"}
+                                      "W7E1", "W7E2", "W6E3", "W9E3"}
     w8 = rt.find_scene("W8 E3 Absorption")
     assert w8.mode == "W8E3" and w8.model == "CornellBox.obj"
     w7 = rt.find_scene("W7 E3 Cornell Box")
