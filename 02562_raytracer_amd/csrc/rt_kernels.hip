@@ -162,6 +162,13 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
     }
     return p;
 }
+// The XCD this wave runs on (HW_REG_XCC_ID, hwreg 20, bits 3:0; 0-7 on MI355X):
+// the k_path work shard.  Any value is correct, only the atomic spread changes.
+__device__ __forceinline__ uint32_t shard_of_wave()
+{
+    return (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | ((3 - 1) << 11)) & 7u;
+}
+
 __device__ __forceinline__ uint32_t fetch_work(uint32_t* ctr, uint32_t lane)
 {
     uint32_t v = 0;
@@ -1247,20 +1254,42 @@ k_path(DevScene S, DevLaunch L)
                 else st = ST_IDLE;
             }
         }
-        // ---- refill idle lanes with new pixels (ballot + mbcnt compaction)
+        // ---- refill idle lanes with new pixels (ballot + mbcnt compaction).
+        //      BVH walk: the slots are dealt round-robin to 8 shards, one per
+        //      XCD, each with its own queue head in its own 128-B line, so the
+        //      refills of 256 CUs do not all meet on one atomic (+22 % on the
+        //      config-3 BVH frame).  The shard is the XCD id read from the
+        //      hardware at each refill; a shard's slots are equal in number and
+        //      interleaved over the frame, so the shards drain together; a wave
+        //      whose home shard is drained moves on to the next ones (restarting
+        //      from home at each refill), so every slot is handed out whatever
+        //      XCDs the waves land on.  The BSP walk keeps one queue: it gained
+        //      nothing from shards, and any shard address here pushed its trip
+        //      loop into spills (tests/test_isa_guard.py).
+        constexpr uint32_t LGSH = TRAV == RT_TRAVERSE_BVH ? 3u : 0u;
+        uint32_t shard = LGSH ? shard_of_wave() : 0u;
+        uint32_t tried = 0;
         for (;;) {
             const uint64_t need = __ballot(st == ST_IDLE && !exhausted);
             if (need == 0) break;
             const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need) - 1u;
             uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(L.work_counter, (uint32_t)__popcll(need));
+            if (lane == leader) {
+                const uint32_t head = atomicAdd(L.work_counter + shard * 32u, (uint32_t)__popcll(need));
+                // a drained shard's head keeps growing with every futile draw:
+                // clamp before the shift so the slot cannot wrap
+                const uint32_t len = (nslots - shard + (1u << LGSH) - 1u) >> LGSH;
+                base = LGSH == 0u ? head : head < len ? (head << LGSH) + shard : nslots;
+            }
             base = __shfl(base, (int)leader, 64);
+            bool ran_out = false;
             if (st == ST_IDLE && !exhausted) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                const uint32_t slot = base + rank;
+                const uint32_t slot = base + (rank << LGSH);
                 if (slot >= nslots) {
-                    exhausted = true;
+                    if (LGSH == 0u) exhausted = true;
+                    else ran_out = true;
                 } else {
                     // chunk-major (unit_order 0): a refill hands out neighbouring
                     // pixels at the same iteration; pixel-major (1): the iterations
@@ -1283,6 +1312,10 @@ k_path(DevScene S, DevLaunch L)
                         start_sample();
                     }
                 }
+            }
+            if (LGSH != 0u && __ballot(ran_out) != 0) {   // this shard is drained (its head only grows)
+                shard = (shard + 1u) & ((1u << LGSH) - 1u);
+                if (++tried == (1u << LGSH)) exhausted = true;
             }
         }
         if (COUNT) {
