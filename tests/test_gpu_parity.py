@@ -160,6 +160,25 @@ def test_bunny_w9e1_bvh_region(rt, gpu):
     check(g, o)
 
 
+@pytest.mark.parametrize("waves,chunk,order", [(1, 1, 1), (3, 3, 0), (32, 1, 0), (32, 5, 1)])
+def test_bvh_work_shards(rt, gpu, waves, chunk, order):
+    # the BVH walk's 8 per-XCD work queues: a wave draws from its XCD's shard,
+    # then from the others once that is drained, so every (pixel, iteration)
+    # unit is rendered exactly once for any grid size and unit shape
+    s = Scene(rt, rt.Mesh.from_obj(model("CornellBoxWithBlocks.obj")), "BVH")
+    try:
+        s.ctx.set_option(rt._ffi.RT_OPT_WAVES_PER_CU, waves)
+        s.ctx.set_option(rt._ffi.RT_OPT_SAMPLE_CHUNK, chunk)
+        s.ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, order)
+        g = s.render_gpu("W7E3", CORNELL_CAM, 120, 100, (4, 6, 100, 90), 0, 7)
+    finally:
+        s.ctx.set_option(rt._ffi.RT_OPT_WAVES_PER_CU, 32)
+        s.ctx.set_option(rt._ffi.RT_OPT_SAMPLE_CHUNK, 1)
+        s.ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, 1)
+    o = s.render_oracle("W7E3", CORNELL_CAM, 120, 100, (4, 6, 100, 90), 0, 7)
+    check(g, o)
+
+
 def test_tileset_unpack_equals_region(rt, cornell_bsp):
     # multi-GPU framebuffer tiling: every rank's packed tiles, gathered and
     # unpacked, reproduce the single-device frame bit for bit (8x8 tiles,

@@ -1,13 +1,13 @@
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/r01_v10
+OUT=gpurun_out/r01_v11
 mkdir -p $OUT
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
-cat $OUT/bench.json
-timeout -k 10 300 python bench.py --trav BVH > $OUT/bench_bvh.json 2> $OUT/bench_bvh.err || { echo "bench rc=$?"; tail -20 $OUT/bench_bvh.err; exit 1; }
-cat $OUT/bench_bvh.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/ks -o ks --output-format csv -- python bench.py --no-cpu-baseline --trav BVH > $OUT/ks.log 2>&1 || { echo "ks rc=$?"; tail -20 $OUT/ks.log; exit 1; }
-find $OUT/ks -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats_bvh.csv \;
-cat $OUT/kernel_stats_bvh.csv
-bash tools/profile_pmc.sh r01_v10_bvh --trav BVH || exit 1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -2 $OUT/pytest_gpu.log
+timeout -k 10 300 python bench.py --trav BVH --no-cpu-baseline > $OUT/bench_bvh.json 2> $OUT/bench_bvh.err || { echo "bench rc=$?"; tail -20 $OUT/bench_bvh.err; exit 1; }
+python tools/bench_brief.py < $OUT/bench_bvh.json
+timeout -k 10 300 python bench.py --config 4 --trav BVH --no-cpu-baseline --steps 1 > $OUT/c4_bvh.json 2> $OUT/c4.err || { echo "c4 rc=$?"; tail -20 $OUT/c4.err; exit 1; }
+python tools/bench_brief.py < $OUT/c4_bvh.json
+timeout -k 10 400 python bench.py --config 5 --trav BVH --spp 64 --no-cpu-baseline --steps 1 > $OUT/c5_bvh.json 2> $OUT/c5.err || { echo "c5 rc=$?"; tail -20 $OUT/c5.err; exit 1; }
+python tools/bench_brief.py < $OUT/c5_bvh.json
 echo done
