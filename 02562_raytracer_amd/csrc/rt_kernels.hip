@@ -252,6 +252,7 @@ struct Trav {
     uint32_t hit_k;
     float beta, gamma;
     uint32_t tos;    // BVH: cached top-of-stack value (node byte offset)
+    uint32_t tos2;   // BVH: cached second entry (valid while node >= 2)
 };
 
 __device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
@@ -491,7 +492,15 @@ __device__ __forceinline__ void bvh_init(Trav& t, float tmin, float tmax)
     t.node = 1;     // top: stack_push_node(0u)
     t.lvl = 0;      // pops
     t.tos = 0u;     // the root's byte offset, cached top of stack
+    t.tos2 = 0u;    // second entry (none yet: its speculative load reads the root again)
 }
+
+// Stack slot of entry i under WGSL index clamping (bvh.wgsl:134-137: node_stack[50]).
+__device__ __forceinline__ uint32_t bvh_slot(uint32_t i) { return i < 50u ? i : 49u; }
+
+#ifndef RT_BVH_TWO_POP
+#define RT_BVH_TWO_POP 1
+#endif
 
 // One trip of a lane through intersect_bvh (bvh.wgsl:154-191), one memory
 // round trip: a lane inside a leaf tests one triangle (its 48-B record), a
@@ -510,11 +519,23 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bvh_base, (short)0, (int)S.bvh_bytes, 0x00020000);
     const bool in_leaf = t.leaf_k != t.leaf_end;
+#if RT_BVH_TWO_POP
+    // a walking lane loads the records of the top two stack entries: when the
+    // first misses, the second is the next pop and is handled in the same trip
+    const uint32_t base = in_leaf ? t.leaf_k : t.tos;
+    const uint32_t base2 = in_leaf ? t.leaf_k + 32u : t.tos2;
+    v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
+    v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
+    v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base2, 0, 0);
+    v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, base2 + 16u, 0, 0);
+    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+#else
     const uint32_t base = in_leaf ? t.leaf_k : t.tos;
     v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
     v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
     v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2));
+#endif
     if (in_leaf) {
         if (COUNT) {
             c.v[C_IDS]++;
@@ -533,6 +554,46 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
         t.leaf_k += 48u;
         if (anyhit & t.found) return true;
     } else {
+#if RT_BVH_TWO_POP
+        // Stack invariant: tos = entry node-1, tos2 = entry node-2 (clamped
+        // slots), so both reads the reference does after a push are exact.
+        // Box tests have no side effect (the slab test ignores the ray
+        // interval), so testing the second entry early changes nothing; it is
+        // only acted on when it is the reference's next pop (the first missed)
+        // and the 1000-pop cap still allows that pop.
+        if (COUNT) c.v[C_POPS]++;
+        t.lvl++;
+        t.node--;
+        uint32_t top = t.tos;
+        bool hit = bb2(inv, o, as_f4(q0), as_f4(q1));
+        uint32_t w0 = q0.w, w1 = q1.w;
+        bool reload = false;   // the new top must come from the stack
+        if (!hit & (t.node != 0u) & (t.lvl < 1000u)) {
+            if (COUNT) c.v[C_POPS]++;
+            t.lvl++;
+            t.node--;
+            top = t.tos2;
+            hit = bb2(inv, o, as_f4(q2), as_f4(q3));
+            w0 = q2.w;
+            w1 = q3.w;
+            reload = true;
+        }
+        if (hit & (w1 != 0u)) {   // leaf: its triangles from the next trip on
+            t.leaf_k = w0;
+            t.leaf_end = w0 + w1;
+        }
+        if (hit & (w1 == 0u)) {   // interior: push left (top + 1), then right
+            const uint32_t n = t.node;
+            bvh_st(stk, dp, bvh_slot(n), top + 32u);
+            bvh_st(stk, dp, bvh_slot(n + 1u), w0);
+            t.node = n + 2u;
+            t.tos = w0;
+            t.tos2 = n >= 49u ? w0 : top + 32u;   // both pushes land in slot 49 from n = 49 on
+        } else {
+            if (t.node != 0u) t.tos = reload ? bvh_ld(stk, dp, bvh_slot(t.node - 1u)) : t.tos2;
+            if (t.node >= 2u) t.tos2 = bvh_ld(stk, dp, bvh_slot(t.node - 2u));
+        }
+#else
         if (COUNT) c.v[C_POPS]++;
         t.lvl++;
         t.node--;
@@ -553,6 +614,7 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
         } else if (t.node != 0u) {
             t.tos = bvh_ld(stk, dp, t.node - 1u < 50u ? t.node - 1u : 49u);
         }
+#endif
     }
     return (t.leaf_k == t.leaf_end) & ((t.lvl >= 1000u) | (t.node == 0u));
 }
