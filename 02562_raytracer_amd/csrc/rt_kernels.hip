@@ -443,6 +443,32 @@ __device__ __forceinline__ f3 bsp_inv(const f3 d) { return V(bsp_inv1(d.x), bsp_
 // intersect_bvh + intersect_bb2, bvh.wgsl:154-191 / 16-83: slab test in axis
 // order y, x, z on [0, 1e27] (ray interval ignored), right child popped first,
 // 1000-pop cap, WGSL index clamping of the 50-entry stack.  One pop per call.
+#ifndef RT_BB2_BRANCHFREE
+#define RT_BB2_BRANCHFREE 1
+#endif
+#if RT_BB2_BRANCHFREE
+// The same predicate without control flow: the swaps and bound updates are
+// selects with the shader's comparisons (NaN compares false, as its ifs do).
+// The early `return false` after an axis needs no flag: t0 only grows and t1
+// only shrinks (neither can become NaN), so t0 > t1 once means t0 > t1 at the end.
+__device__ __forceinline__ void bb2_axis(float tn, float tf, float& t0, float& t1)
+{
+    const bool sw = tn > tf;
+    const float lo = sw ? tf : tn, hi = sw ? tn : tf;
+    t0 = lo > t0 ? lo : t0;
+    t1 = hi < t1 ? hi : t1;
+}
+__device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, const float4 b)
+{
+    float t0 = 0.0f, t1 = 1e27f;
+    const f3 nr = mul(sub(V(a.x, a.y, a.z), o), inv);
+    const f3 fr = mul(sub(V(b.x, b.y, b.z), o), inv);
+    bb2_axis(nr.y, fr.y, t0, t1);
+    bb2_axis(nr.x, fr.x, t0, t1);
+    bb2_axis(nr.z, fr.z, t0, t1);
+    return !(t0 > t1);
+}
+#else
 __device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, const float4 b)
 {
     float t0 = 0.0f, t1 = 1e27f;
@@ -464,6 +490,7 @@ __device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, co
     if (tf < t1) t1 = tf;
     return !(t0 > t1);
 }
+#endif
 
 // BVH stack split: entries [0, K) in LDS ([slot][thread], 4 B), entries [K, 50)
 // in a per-lane global region ([slot - K][lane] across the grid) -- a walk
