@@ -1,8 +1,10 @@
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/r01v14
+OUT=gpurun_out/r01v17
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests/test_gpu_bvh_stack.py tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "bvh or BVH" > $OUT/bvh_tests.log 2>&1 || { echo "tests rc=$?"; tail -30 $OUT/bvh_tests.log; exit 1; }
-tail -1 $OUT/bvh_tests.log
-bash tools/ab.sh $OUT/ab.txt "--trav BVH" 2pop bf 2pop bf || exit 1
-cat $OUT/ab.txt | cut -c1-80
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -30 $OUT/pytest_gpu.log; exit 1; }
+tail -1 $OUT/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $OUT/smoke.log; exit 1; }
+tail -1 $OUT/smoke.log
+timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench.json | cut -c1-400
