@@ -1,10 +1,12 @@
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/r01v17
+OUT=gpurun_out/r01v18b
 mkdir -p $OUT
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -30 $OUT/pytest_gpu.log; exit 1; }
-tail -1 $OUT/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $OUT/smoke.log; exit 1; }
-tail -1 $OUT/smoke.log
-timeout -k 10 300 python bench.py > $OUT/bench.json 2> $OUT/bench.err || { echo "bench rc=$?"; tail -20 $OUT/bench.err; exit 1; }
-cat $OUT/bench.json | cut -c1-400
+( while sleep 20; do date >> $OUT/heartbeat.txt; done ) &
+HB=$!
+trap "kill $HB" EXIT
+for a in "5 BVH" "4 BSP" "2 BSP"; do
+  set -- $a
+  timeout -k 10 500 python -u bench.py --config $1 --trav $2 --no-cpu-baseline > $OUT/c$1_$2.json 2> $OUT/c$1_$2.err || { echo "config $1 $2 rc=$?"; tail -20 $OUT/c$1_$2.err; exit 1; }
+  python tools/bench_brief.py < $OUT/c$1_$2.json | cut -c1-100
+done
