@@ -291,10 +291,6 @@ __device__ __forceinline__ TraceOut trav_out(const Trav& t) { return TraceOut{t.
 // m >= 1 always (a zero argument would be undefined: no clamp instruction)
 __device__ __forceinline__ uint32_t heap_depth(uint32_t m) { return 31u - (uint32_t)__builtin_clz(m); }
 
-#ifndef RT_BSP_TREELET_POP
-#define RT_BSP_TREELET_POP 0
-#endif
-
 __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 {
     if (t.lvl == 0) return true;   // `branch_lvl == 0u` -> return false (miss)
@@ -423,31 +419,6 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             t.leaf_end = n.y + (n.x >> 2);   // 48 * count
             pop = (n.x >> 2) == 0u;
         }
-#if RT_BSP_TREELET_POP
-        // An empty leaf whose pop target lies in this treelet (the far child
-        // of a push at its level 0 or 1): pop now and visit the target from
-        // the loaded data -- the same operations in the same order, one trip
-        // earlier.
-        if (pop & (t.lvl != 0u)) {
-            const uint32_t pd = heap_depth(t.lvl);
-            if (pd >= dep) {
-                bsp_pop(stk, t);
-                pop = false;
-                const uint32_t x = t.node;
-                const v4u g = (x & 2u) ? q3 : q2;
-                const uint2 nx = pd == dep ? ((x & 1u) ? make_uint2(q1.x, q1.y) : make_uint2(q0.z, q0.w))
-                                           : ((x & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y));
-                if ((nx.x & 3u) == 3u) {
-                    if (COUNT) c.v[C_LEAF]++;
-                    t.leaf_k = nx.y;
-                    t.leaf_end = nx.y + (nx.x >> 2);
-                    pop = (nx.x >> 2) == 0u;
-                } else if (RT_BSP_TREELET_POP == 1) {
-                    t.node = bsp_decide<COUNT>(stk, nx, x, pd + 1u, o, d, inv, t, c);
-                }   // (2: an interior target is walked from the next trip, as after any pop)
-            }
-        }
-#endif
     }
     if (pop) done = bsp_pop(stk, t);
     return done;

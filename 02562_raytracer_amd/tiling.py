@@ -1,6 +1,6 @@
 """Framebuffer tiling across ranks: one process per GPU, each
 renders the interleaved 8x8 tiles t = l*nranks + rank (rt_render_tiles), the
-packed tiles are all-gathered, and rank 0 scatters them into the frame
+packed tiles are gathered to rank 0, and rank 0 scatters them into the frame
 (rt_unpack_tiles).  The gather is the only collective of the path.
 
 The packed layout (include/rt.h rt_render_tiles): local tile l occupies pixels
@@ -44,20 +44,26 @@ def unpack_numpy(width, height, nranks, local_tiles, packed_accum, packed_ids):
 
 
 def gather_tiles(dist, acc_local, ids_local, acc_all, ids_all):
-    """All-gather the ranks' packed tiles into rank-major buffers (every rank
-    receives all; the frame is assembled on rank 0).  RCCL (backend "nccl")
-    gathers straight into the flat tensors; gloo (CPU tests) through a list."""
-    if dist.get_backend() == "nccl":
-        dist.all_gather_into_tensor(acc_all, acc_local)
-        dist.all_gather_into_tensor(ids_all, ids_local)
-        return
+    """Gather the ranks' packed tiles to rank 0, rank-major into acc_all /
+    ids_all (None on the other ranks): SURVEY.md 8(e)'s gather-to-root -- only
+    the rank that assembles the frame receives.  RCCL (backend "nccl") gathers
+    device tensors in place (point-to-point over xGMI); gloo through host memory
+    (the CPU tests, and the one-GPU rehearsal of the device path)."""
     world = dist.get_world_size()
-    if acc_local.is_cuda:   # gloo rehearsal of the device path: through host memory
-        ha, hi = acc_all.cpu(), ids_all.cpu()
-        dist.all_gather(list(ha.chunk(world)), acc_local.cpu())
-        dist.all_gather(list(hi.chunk(world)), ids_local.cpu())
-        acc_all.copy_(ha)
-        ids_all.copy_(hi)
+    root = dist.get_rank() == 0
+    if dist.get_backend() == "nccl":
+        dist.gather(acc_local, list(acc_all.chunk(world)) if root else None, dst=0)
+        dist.gather(ids_local, list(ids_all.chunk(world)) if root else None, dst=0)
         return
-    dist.all_gather(list(acc_all.chunk(world)), acc_local)
-    dist.all_gather(list(ids_all.chunk(world)), ids_local)
+    if acc_local.is_cuda:   # gloo rehearsal of the device path: through host memory
+        ha = acc_all.cpu() if root else None
+        hi = ids_all.cpu() if root else None
+        dist.gather(acc_local.cpu(), list(ha.chunk(world)) if root else None, dst=0)
+        dist.gather(ids_local.cpu(), list(hi.chunk(world)) if root else None, dst=0)
+        if root:
+            acc_all.copy_(ha)
+            ids_all.copy_(hi)
+        return
+    dist.gather(acc_local, list(acc_all.chunk(world)) if root else None, dst=0)
+    dist.gather(ids_local, list(ids_all.chunk(world)) if root else None, dst=0)
+

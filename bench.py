@@ -29,6 +29,12 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 L2_PEAK_GBS = 34500.0   # aggregate L2 (8 XCDs x 4 MiB), MI355X_MICROARCH.md "L2 (per XCD)"
+# VALU issue: a wave64 VALU instruction issues over 2 cycles on its SIMD
+# (MI355X_MICROARCH.md "issues each VALU instruction over 2 cycles"): 256 CUs x 4
+# SIMDs x 2.4 GHz (max clock) / 2 = wave-instructions per second, chip-wide
+NUM_CUS, SIMDS_PER_CU, MAX_CLOCK_GHZ = 256, 4, 2.4
+VALU_PEAK_GINSTS = NUM_CUS * SIMDS_PER_CU * MAX_CLOCK_GHZ / 2.0
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
 METRIC = "Mrays/sec primary+shadow at 1920x1080; achieved HBM GB/s vs peak"
 
 
@@ -64,7 +70,10 @@ def cpu_baseline(wl, trav, mesh, accel, spp, W, H, budget_s):
         nodes, tids = accel.arrays()
         osc = O.SceneRef(om, None, O.OracleBvh(nodes, tids), env=wl.env)
     u = O.make_uniform(*wl.camera, W, H)
-    cores = min(16, os.cpu_count() or 1)
+    # the threads this process may use: the GPU box gives each GPU a 16-thread
+    # share of the host (it sets OMP_NUM_THREADS=16; os.cpu_count() there reports
+    # the whole machine, which other jobs share); here, every core of the container
+    cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or len(os.sched_getaffinity(0))
     region = (0, 0, W, H)
     acc = None
     rays = 0
@@ -80,6 +89,52 @@ def cpu_baseline(wl, trav, mesh, accel, spp, W, H, budget_s):
     return {"value": rays / el / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
             "sample": f"CPU oracle (C restatement of {wl.mode.lower()}.wgsl+{trav.lower()}.wgsl, pthreads), the same "
                       f"{W}x{H} frame, first {it} of its {spp} spp, {el:.1f} s"}
+
+
+def pmc_key(W, H, spp, trav, world, config):
+    return f"{W}x{H}x{spp}_{trav}_n{world}" + ("" if config == 3 else f"_c{config}")
+
+
+def roofline(key, kern_ms, alg_bytes, config, kernel):
+    """Roofline of the dominant kernel.  Counter figures per launch (HBM bytes,
+    VALU wave-instructions) come from the committed PMC summary of the same
+    workload (profiles/pmc_summary.json, tools/pmc_summary.py; its `source` names
+    the rocprofv3 passes); the time is this run's HIP-event kernel time.
+      * config 5 (10M triangles, 1.5 GB of BSP: the scene does not fit in
+        cache): bound "hbm", frac = counter HBM bytes / time / 8 TB/s;
+      * configs 2-4 (cache-resident scenes): bound "valu-issue", frac = VALU
+        wave-instructions / time / the chip's VALU issue rate -- the limit the
+        counters show (DESIGN.md "What bounds it"); the HBM fraction is given beside.
+    The SURVEY 8(d) algorithmic bytes (reference layout) over the kernel time is a
+    diagnostic ("algorithmic"): the bytes stay in L2/MALL, so against HBM it can
+    exceed 1 and is never reported as the HBM fraction."""
+    s = kern_ms / 1e3
+    pmc = None
+    if os.path.exists(PMC_SUMMARY):
+        with open(PMC_SUMMARY) as f:
+            pmc = json.load(f).get(key)
+    alg = {"bytes_per_launch": int(alg_bytes), "achieved": round(alg_bytes / s / 1e9, 1), "unit": "GB/s",
+           "l2_peak": L2_PEAK_GBS, "l2_frac": round(alg_bytes / s / 1e9 / L2_PEAK_GBS, 4)}
+    r = {"kernel": kernel, "kernel_ms": round(kern_ms, 3), "algorithmic": alg, "pmc": None, "traffic": None}
+    if pmc is None:
+        r.update({"bound": "unmeasured", "achieved": None, "peak": None, "unit": None, "frac": None,
+                  "note": f"no PMC summary for {key} in profiles/pmc_summary.json"})
+        return r
+    hbm_gbs = pmc["hbm_bytes_per_launch"] / s / 1e9
+    valu = pmc["valu_insts_per_launch"] / s / 1e9
+    r["traffic"] = int(pmc["hbm_bytes_per_launch"])
+    r["hbm"] = {"achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(hbm_gbs / HBM_PEAK_GBS, 4)}
+    r["valu_issue"] = {"achieved": round(valu, 1), "peak": round(VALU_PEAK_GINSTS, 1),
+                       "unit": "G wave64 VALU instr/s", "frac": round(valu / VALU_PEAK_GINSTS, 4)}
+    r["pmc"] = {k: pmc[k] for k in ("source", "kernel_ms_profiled", "l2_hit_rate", "valu_lane_util", "wait_frac",
+                                    "write_bytes_per_launch", "fetch_bytes_per_launch") if k in pmc}
+    prim = r["hbm"] if config == 5 else r["valu_issue"]
+    r.update({"bound": "hbm" if config == 5 else "valu-issue", "achieved": prim["achieved"], "peak": prim["peak"],
+              "unit": prim["unit"], "frac": prim["frac"]})
+    if max(r["hbm"]["frac"], r["valu_issue"]["frac"]) > 1.0:   # a summary of another kernel build
+        r.update({"bound": "unmeasured", "frac": None, "note": f"PMC summary for {key} does not match this kernel"})
+    return r
 
 
 def all_reduce(dist, t, op):
@@ -110,6 +165,8 @@ def main():
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)
     ap.add_argument("--min-half-lanes", type=int, default=None)
+    ap.add_argument("--dump-frame", default=None,
+                    help="rank 0 saves the last step's assembled frame (accum + ids) to this .npz")
     args = ap.parse_args()
 
     import torch
@@ -174,7 +231,8 @@ def main():
     lt = rt.local_tiles(W, H, world)
     acc_local = torch.empty((lt * 64, 4), dtype=torch.float32, device=dev)
     ids_local = torch.empty((lt * 64,), dtype=torch.int32, device=dev)
-    if world > 1:
+    acc_all = ids_all = None
+    if world > 1 and rank == 0:   # gather-to-root: only rank 0 receives the packed tiles
         acc_all = torch.empty((world * lt * 64, 4), dtype=torch.float32, device=dev)
         ids_all = torch.empty((world * lt * 64,), dtype=torch.int32, device=dev)
     frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
@@ -240,17 +298,12 @@ def main():
 
     value = rays[0] * args.steps / elapsed / 1e6
     if rank == 0:
-        # roofline of the dominant kernel (k_path<mode, traversal>): bytes of one launch
-        # on one GPU / its average HIP-event duration
+        # roofline of the dominant kernel (k_path<mode, traversal>): one launch on one GPU
         bytes_per_launch = rays[4] / world / max(1, launches_per_step)
-        achieved = bytes_per_launch / (kern_ms / 1e3) / 1e9
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(pmc):
-            with open(pmc) as f:
-                p = json.load(f)
-            key = f"{W}x{H}x{spp}_{trav}_n{world}" + ("" if args.config == 3 else f"_c{args.config}")
-            traffic = p.get(key)
+        roof = roofline(pmc_key(W, H, spp, trav, world, args.config), kern_ms, bytes_per_launch, args.config,
+                        f"k_path<{wl.mode},{trav}>")
+        roof["launches_per_step"] = launches_per_step
+        roof["render_ms"] = round(render_ms, 3)
         cpu = None
         if not args.no_cpu_baseline and world == 1:
             cpu = cpu_baseline(wl, trav, mesh, accel, spp, W, H, args.cpu_budget)
@@ -261,15 +314,10 @@ def main():
             "config": {"workload": f"config {wl.number}: {wl.name} ({mesh.ntris} tris), "
                                    f"{trav}{' D20/leaf4' if trav == 'BSP' else ' leaf4'}, {W}x{H}, {spp} spp/step",
                        "resolution": [W, H], "spp": spp, "traversal": trav, "ntris": mesh.ntris, "mode": wl.mode,
-                       "parallelism": f"tiles8x8/{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": f"k_path<{wl.mode},{trav}>", "kernel_ms": round(kern_ms, 3),
-                         "launches_per_step": launches_per_step, "render_ms": round(render_ms, 3),
-                         "algorithmic_bytes_per_launch": int(bytes_per_launch),
-                         # the scene is cache-resident: the same bytes against the chip's
-                         # aggregate L2 bandwidth (MI355X_MICROARCH.md: ~34.5 TB/s)
-                         "l2_peak": L2_PEAK_GBS, "l2_frac": round(achieved / L2_PEAK_GBS, 4)},
+                       "parallelism": f"tiles8x8/{world}",
+                       "world_size": dist.get_world_size() if world > 1 else 1,
+                       "backend": dist.get_backend() if world > 1 else None},
+            "roofline": roof,
             "cpu_baseline": cpu,
             "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},
             "traversal_per_launch": {k: detail[k] for k in ("node_interior", "node_leaf", "bvh_pops", "tri_tests",
@@ -282,6 +330,8 @@ def main():
             "setup_s": round(setup_s, 3),
         }
         print(json.dumps(line), flush=True)
+        if args.dump_frame:
+            np.savez(args.dump_frame, accum=frame.cpu().numpy(), ids=frame_ids.cpu().numpy().view(np.uint32))
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

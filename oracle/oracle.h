@@ -141,6 +141,19 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
 int or_trace_one(const or_scene* s, int trav, int face_normals, const float o[3], const float d[3],
                  float tmin, float tmax, uint32_t* tri, float* dist);
 
+/* fs_main's camera ray (w7e3.wgsl:211-228 with uv of pixel (x, y), project.wgsl:131-148
+ * jitter): origin and direction, as every render mode builds it. */
+void or_camera_ray(const or_uniform* u, uint32_t x, uint32_t y, float jx, float jy, float o[3], float d[3]);
+
+/* one ray query as w6e1/project's fs_main issues it (w6e1.wgsl:160-175): with clip,
+ * the root-AABB clip intersect_min_max (aabb.wgsl:8-31) first; then the walk.
+ * Returns -1 when the clip rejects the ray, else hit (1) / miss (0); reports
+ * the ray interval the walk leaves behind (bsp.wgsl mutates it in place) and
+ * the triangle ids in the order they were tested (up to cap; *ntested = all). */
+int or_trace_query(const or_scene* s, int trav, int clip, const float o[3], const float d[3], float tmin,
+                   float tmax, uint32_t* tri, float* dist, float* out_tmin, float* out_tmax, uint32_t* tested,
+                   uint32_t cap, uint32_t* ntested);
+
 /* brute-force closest hit over all triangles (w5e2-style loop, no accel). */
 int or_trace_brute(const or_scene* s, const float o[3], const float d[3], float tmin, float tmax,
                    uint32_t* tri, float* dist);

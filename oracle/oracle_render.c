@@ -59,6 +59,8 @@ typedef struct {
     const float* jitter;
     int mode, trav;
     or_counts c;
+    uint32_t* log;       /* or_trace_query: triangle ids in test order (NULL: off) */
+    uint32_t log_cap, log_n;
 } Ctx;
 
 /* ------------------------------------------------------------ PRNG (w7e3.wgsl:141-172) */
@@ -86,6 +88,10 @@ static int tri_test(Ctx* C, Ray* r, Hit* h, uint32_t v, int face_normals)
 {
     const or_scene* s = C->s;
     C->c.tri_tests++;
+    if (C->log) {
+        if (C->log_n < C->log_cap) C->log[C->log_n] = v;
+        C->log_n++;
+    }
     const uint32_t* ix = s->idx + 4 * (size_t)v;
     v3 v0 = load3(s->pos + 4 * (size_t)ix[0]);
     v3 v1 = load3(s->pos + 4 * (size_t)ix[1]);
@@ -1512,6 +1518,48 @@ int or_trace_one(const or_scene* s, int trav, int face_normals, const float o[3]
     *tri = hit ? h.tri : 0xFFFFFFFFu;
     *dist = hit ? h.dist : 0.0f;
     return hit;
+}
+
+void or_camera_ray(const or_uniform* u, uint32_t x, uint32_t y, float jx, float jy, float o[3], float d[3])
+{
+    Cam cam = make_cam(u);
+    float ux, uy;
+    pixel_uv(u, x, y, &ux, &uy);
+    v3 dir = cam_dir(&cam, ux, uy, jx, jy);
+    o[0] = cam.e.x;
+    o[1] = cam.e.y;
+    o[2] = cam.e.z;
+    d[0] = dir.x;
+    d[1] = dir.y;
+    d[2] = dir.z;
+}
+
+int or_trace_query(const or_scene* s, int trav, int clip, const float o[3], const float d[3], float tmin,
+                   float tmax, uint32_t* tri, float* dist, float* out_tmin, float* out_tmax, uint32_t* tested,
+                   uint32_t cap, uint32_t* ntested)
+{
+    Ctx C;
+    memset(&C, 0, sizeof C);
+    C.s = s;
+    C.trav = trav;
+    C.log = tested;
+    C.log_cap = tested ? cap : 0;
+    Ray r;
+    r.origin = load3(o);
+    r.direction = load3(d);
+    r.tmin = tmin;
+    r.tmax = tmax;
+    Hit h;
+    memset(&h, 0, sizeof h);
+    int hit = 0, clipped = 0;
+    if (clip && !intersect_min_max(s->aabb, &r)) clipped = 1;   /* w6e1.wgsl:165-168: the sample ends */
+    if (!clipped) hit = trace(&C, &r, &h, 1);
+    *tri = hit ? h.tri : 0xFFFFFFFFu;
+    *dist = hit ? h.dist : 0.0f;
+    *out_tmin = r.tmin;
+    *out_tmax = r.tmax;
+    if (ntested) *ntested = C.log_n;
+    return clipped ? -1 : hit;
 }
 
 int or_trace_brute(const or_scene* s, const float o[3], const float d[3], float tmin, float tmax,

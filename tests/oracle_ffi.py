@@ -98,6 +98,10 @@ def lib():
                                 f32p, u32p, C.POINTER(Counts), C.c_int]
         L.or_trace_one.argtypes = [C.POINTER(Scene), C.c_int, C.c_int, f32p, f32p, C.c_float, C.c_float,
                                    u32p, f32p]
+        L.or_camera_ray.argtypes = [C.POINTER(Uniform), C.c_uint32, C.c_uint32, C.c_float, C.c_float, f32p, f32p]
+        L.or_camera_ray.restype = None
+        L.or_trace_query.argtypes = [C.POINTER(Scene), C.c_int, C.c_int, f32p, f32p, C.c_float, C.c_float,
+                                     u32p, f32p, f32p, f32p, u32p, C.c_uint32, u32p]
         L.or_trace_brute.argtypes = [C.POINTER(Scene), f32p, f32p, C.c_float, C.c_float, u32p, f32p]
         for n in ("or_det_sinf", "or_det_cosf", "or_det_acosf"):
             getattr(L, n).argtypes = [C.c_float]
@@ -285,6 +289,32 @@ def trace_one(scene, trav, o, d, tmin, tmax, face_normals=1):
     hit = L.or_trace_one(C.byref(scene.s), TRAVS[trav], face_normals, o.ctypes.data_as(f32p),
                          d.ctypes.data_as(f32p), tmin, tmax, C.byref(tri), C.byref(dist))
     return bool(hit), tri.value, dist.value
+
+
+def camera_ray(uniform, x, y, jx=0.0, jy=0.0):
+    """fs_main's camera ray for pixel (x, y): (origin, direction) float32[3]."""
+    o = np.zeros(3, dtype=np.float32)
+    d = np.zeros(3, dtype=np.float32)
+    lib().or_camera_ray(C.byref(uniform), x, y, jx, jy, o.ctypes.data_as(f32p), d.ctypes.data_as(f32p))
+    return o, d
+
+
+def trace_query(scene, trav, o, d, tmin, tmax, clip=False, cap=4096):
+    """One walk as w6e1/project issue it (optional root-AABB clip first).
+    Returns dict(status -1 clipped / 0 miss / 1 hit, tri, dist, tmin, tmax,
+    tested = triangle ids in test order)."""
+    L = lib()
+    o = np.asarray(o, dtype=np.float32)
+    d = np.asarray(d, dtype=np.float32)
+    tri, n = C.c_uint32(), C.c_uint32()
+    dist, t0, t1 = C.c_float(), C.c_float(), C.c_float()
+    log = np.zeros(cap, dtype=np.uint32)
+    st = L.or_trace_query(C.byref(scene.s), TRAVS[trav], int(clip), o.ctypes.data_as(f32p), d.ctypes.data_as(f32p),
+                          tmin, tmax, C.byref(tri), C.byref(dist), C.byref(t0), C.byref(t1),
+                          log.ctypes.data_as(u32p), cap, C.byref(n))
+    assert n.value <= cap
+    return {"status": st, "tri": tri.value, "dist": dist.value, "tmin": t0.value, "tmax": t1.value,
+            "tested": log[:n.value].copy()}
 
 
 def trace_brute(scene, o, d, tmin, tmax):

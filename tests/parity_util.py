@@ -68,7 +68,10 @@ class Scene:
 
 
 def compare(gpu, ora, what=""):
-    """Returns (max abs radiance diff, #bit mismatches, #id mismatches)."""
+    """Returns (max abs radiance diff, #bit mismatches, #id mismatches).  The
+    L-inf is infinite when the two sides disagree on a non-finite value: NaN
+    against a number, an infinity against a finite value, or +inf against -inf
+    (such differences vanish from a finite-only max)."""
     ga, gi, gc = gpu
     oa, oi, oc = ora
     diff = np.abs(ga.astype(np.float64) - oa.astype(np.float64))
@@ -76,6 +79,7 @@ def compare(gpu, ora, what=""):
     linf = float(diff[finite].max()) if finite.any() else 0.0
     both_nan = np.isnan(ga) & np.isnan(oa)   # NaN payload/sign is not a value (x86 0/0 = -qNaN)
     nan_mismatch = int((np.isnan(ga) != np.isnan(oa)).sum())
+    inf_mismatch = int(((np.isinf(ga) | np.isinf(oa)) & (ga != oa)).sum())
     bits = int(((ga.view(np.uint32) != oa.view(np.uint32)) & ~both_nan).sum())
     idm = int((gi != oi).sum())
-    return linf + (np.inf if nan_mismatch else 0.0), bits, idm
+    return linf + (np.inf if nan_mismatch or inf_mismatch else 0.0), bits, idm

@@ -65,8 +65,10 @@ def _worker(rank, nranks, port, outdir):
         acc, ids = _render_rank(rank, nranks, lt)
         acc_l = torch.from_numpy(acc)
         ids_l = torch.from_numpy(ids.view(np.int32))
-        acc_all = torch.empty((nranks * lt * 64, 4), dtype=torch.float32)
-        ids_all = torch.empty((nranks * lt * 64,), dtype=torch.int32)
+        acc_all = ids_all = None   # gather-to-root: only rank 0 receives
+        if rank == 0:
+            acc_all = torch.empty((nranks * lt * 64, 4), dtype=torch.float32)
+            ids_all = torch.empty((nranks * lt * 64,), dtype=torch.int32)
         tiling.gather_tiles(dist, acc_l, ids_l, acc_all, ids_all)
         if rank == 0:
             frame, fids = tiling.unpack_numpy(W, H, nranks, lt, acc_all.numpy(), ids_all.numpy().view(np.uint32))

@@ -3,8 +3,10 @@ counter (summed over the counter's dimensions), plus derived figures.
 
   pmc_summary.py <dir> [kernel-substring] [--out FILE] [--traffic KEY]
 
---traffic KEY records the kernel's HBM bytes per launch in
-profiles/pmc_traffic.json under KEY (bench.py reads it for roofline.traffic).
+--summary KEY records the kernel's per-launch counter figures in
+profiles/pmc_summary.json under KEY (bench.py's roofline reads them): HBM bytes,
+VALU wave-instructions, L2 hit rate, VALU lane utilisation, wait fraction, and
+`source` = the directory of the passes (commit it under profiles/).
 HBM bytes = 2 x FETCH_SIZE + WRITE_SIZE (KiB units): MI355X_MICROARCH.md
 "HBM / rocprofv3": on gfx950 FETCH_SIZE reports half the bytes of wide reads.
 """
@@ -54,7 +56,8 @@ if __name__ == "__main__":
     ap.add_argument("dir")
     ap.add_argument("kernel", nargs="?")
     ap.add_argument("--out")
-    ap.add_argument("--traffic")
+    ap.add_argument("--summary")
+    ap.add_argument("--source", help="profiles/ path recorded as the summary's source")
     a = ap.parse_args()
     res = load(a.dir, a.kernel)
     out = {k: {"counters": c, "derived": derived(c)} for k, c in res.items()}
@@ -63,13 +66,22 @@ if __name__ == "__main__":
     if a.out:
         with open(a.out, "w") as f:
             f.write(txt + "\n")
-    if a.traffic:
+    if a.summary:
         if len(res) != 1:
-            raise SystemExit(f"--traffic needs exactly one kernel, got {list(res)}")
-        (c,) = res.values()
-        path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+            raise SystemExit(f"--summary needs exactly one kernel, got {list(res)}")
+        (kname, c), = res.items()
+        d = derived(c)
+        ent = {"kernel": kname, "source": a.source or a.dir,
+               "hbm_bytes_per_launch": int(d["hbm_bytes_per_launch"]),
+               "fetch_bytes_per_launch": int(2.0 * c["FETCH_SIZE"] * 1024.0),
+               "write_bytes_per_launch": int(c["WRITE_SIZE"] * 1024.0),
+               "valu_insts_per_launch": int(c["SQ_INSTS_VALU"])}
+        for k in ("l2_hit_rate", "valu_lane_util", "wait_frac", "salu_per_valu", "l1_hit_rate"):
+            if k in d:
+                ent[k] = round(d[k], 4)
+        path = os.path.join(ROOT, "profiles", "pmc_summary.json")
         cur = json.load(open(path)) if os.path.exists(path) else {}
-        cur[a.traffic] = int(derived(c)["hbm_bytes_per_launch"])
+        cur[a.summary] = ent
         with open(path, "w") as f:
             json.dump(cur, f, indent=1, sort_keys=True)
             f.write("\n")
