@@ -349,7 +349,7 @@ uint32_t rt_tileset_local_tiles(uint32_t width, uint32_t height, uint32_t nranks
 int rt_frame_rgba8(rt_ctx* ctx, const float* accum_rgba32f, uint32_t npix, uint8_t* frame_rgba8);
 
 /* Scatter gathered packed buffers (nranks x local_tiles x 64 px, rank-major as
- * produced by an all-gather) into a row-major W x H frame, on the context's
+ * a gather to the root produces them) into a row-major W x H frame, on the context's
  * stream.  Either pair of pointers may be NULL. */
 int rt_unpack_tiles(rt_ctx* ctx, uint32_t width, uint32_t height, uint32_t nranks,
                     const float* packed_accum, const uint32_t* packed_ids,
