@@ -16,9 +16,9 @@
 //                 emit_lbvh call; then k_bottom_up per level (subtree sizes and
 //                 boxes: leaf = fold of its primitive boxes in order, internal =
 //                 child0's box including child1's)
-//   upper_tree    the <= 4096 treelet roots' boxes go to the host, which runs
-//                 the reference's median-split collapse (rthost::bvh_upper_tree,
-//                 shared with host_bvh.cpp) and the DFS offsets of the flatten
+//   upper_tree    k_upper_tree: the reference's median-split collapse over the
+//                 <= 4096 treelet roots in one workgroup (a bitonic sort per
+//                 level), the DFS offsets of the roots and the upper nodes' records
 //   flattening    k_top_down per level (DFS index of every node: left child
 //                 = parent+1, right = parent+1+size(left)), k_write_nodes, the
 //                 upper nodes, the GpuNode::new(root box) filler of the
@@ -424,20 +424,248 @@ __global__ void __launch_bounds__(256) k_write_nodes(const Ctl* ctl, const BNode
     }
 }
 
-__global__ void __launch_bounds__(256) k_fill_nodes(rt_gpu_node* out, uint32_t n, rt_gpu_node filler)
-{
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) out[i] = filler;
-}
-
 __global__ void __launch_bounds__(256) k_scatter_nodes(const rt_gpu_node* src, const uint32_t* at, uint32_t n,
                                                        rt_gpu_node* out)
 {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) out[at[i]] = src[i];
 }
 
-__global__ void __launch_bounds__(256) k_set_dfs(const uint32_t* dfs, uint32_t n, BNode* pool)
+// ------------------------------------------------------------ upper tree (device)
+// collapse_build_nodes_recursive + mid_partition (hlbvh.rs:252-291) over the
+// <= 4096 treelet roots, in one workgroup.  The recursion's segments are the
+// nodes of the midpoint tree over positions [0, n) (children [lo, mid) and
+// [mid, hi), mid = lo + (hi - lo) / 2): its shape does not depend on the data.
+// Level by level, every segment with >= 2 members takes the longest axis of
+// its members' centroid bound (bbox.rs longest_axis) and is sorted stably by
+// the centroid on that axis (f32::total_cmp order; ties keep the order the
+// level above left, as the host builder's stable_sort does): one bitonic sort
+// of (segment start, key, position) per level.  Then, from the final order:
+//   * pre-order DFS index of node (lo, hi) at depth d with r right turns on its
+//     path: prefix(lo) + d + lo - r, prefix = the subtree sizes of the leaves
+//     before it (each right turn passes a left sibling subtree of size - 1
+//     internal nodes; the ancestors are the other d);
+//   * internal node <-> the boundary m = its mid (1 <= m < n, one each);
+//   * boxes bottom-up: child0's box including child1's (rt_minf keeps the left
+//     operand on ties, so a fold is the leftmost minimum in position order).
+// Bit-identical to rthost::bvh_upper_tree for meshes without NaN coordinates
+// (tests/test_gpu_build.py).
+namespace upper {
+constexpr uint32_t kMax = 4096;   // treelets: 12-bit Morton prefixes
+__device__ __forceinline__ uint32_t fkey(float f)   // f32::total_cmp order (-0 < +0)
 {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) pool[i].dfs = dfs[i];
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+__device__ __forceinline__ float funkey(uint32_t k)
+{
+    return __uint_as_float((k & 0x80000000u) ? (k & 0x7FFFFFFFu) : ~k);
+}
+struct Seg {
+    uint32_t lo, hi, depth, rights, ord;
+};
+// the deepest segment containing position p at depth <= lev
+__device__ __forceinline__ Seg descend(uint32_t n, uint32_t p, uint32_t lev)
+{
+    Seg g{0u, n, 0u, 0u, 0u};
+    while (g.depth < lev && g.hi - g.lo >= 2u) {
+        const uint32_t mid = g.lo + (g.hi - g.lo) / 2u;
+        g.ord <<= 1;
+        if (p < mid) {
+            g.hi = mid;
+        } else {
+            g.lo = mid;
+            g.ord |= 1u;
+            g.rights++;
+        }
+        g.depth++;
+    }
+    return g;
+}
+// the internal node whose mid is m (1 <= m < n)
+__device__ __forceinline__ Seg node_of(uint32_t n, uint32_t m)
+{
+    Seg g{0u, n, 0u, 0u, 0u};
+    for (;;) {
+        const uint32_t mid = g.lo + (g.hi - g.lo) / 2u;
+        if (mid == m) return g;
+        if (m < mid) {
+            g.hi = mid;
+        } else {
+            g.lo = mid;
+            g.rights++;
+        }
+        g.depth++;
+    }
+}
+__device__ __forceinline__ float centre(const BNode& b, uint32_t k) { return (b.mn[k] + b.mx[k]) * 0.5f; }
+}  // namespace upper
+
+__global__ void __launch_bounds__(1024) k_upper_tree(const Ctl* ctl, BNode* pool, rt_gpu_node* up, uint32_t* up_at,
+                                                     float* root_box)
+{
+    using namespace upper;
+    __shared__ uint32_t perm[kMax], pre[kMax + 1];
+    // sort phase: keys + per-segment centroid bounds; output phase: node boxes
+    __shared__ __attribute__((aligned(16))) uint8_t pool_lds[kMax * 24];
+    uint64_t* key = reinterpret_cast<uint64_t*>(pool_lds);                     // [kMax]
+    uint32_t* bmn = reinterpret_cast<uint32_t*>(pool_lds + kMax * 8);          // [3][kMax/2]
+    uint32_t* bmx = bmn + 3 * (kMax / 2);
+    float* box = reinterpret_cast<float*>(pool_lds);                           // [kMax-1][6]
+    const uint32_t tid = threadIdx.x, n = ctl->ntreelets;
+    if (n == 0u) return;
+    uint32_t np = 1, L = 0;
+    while (np < n) {
+        np <<= 1;
+        L++;
+    }
+    for (uint32_t p = tid; p < n; p += 1024u) perm[p] = p;
+    __syncthreads();
+    for (uint32_t lev = 0; lev < L; lev++) {
+        for (uint32_t i = tid; i < 3u * (kMax / 2); i += 1024u) {
+            bmn[i] = 0xFFFFFFFFu;
+            bmx[i] = 0u;
+        }
+        __syncthreads();
+        for (uint32_t p = tid; p < n; p += 1024u) {   // centroid bounds (Bbox::include_vertex)
+            const Seg g = descend(n, p, lev);
+            if (g.hi - g.lo >= 2u) {
+                const BNode& b = pool[perm[p]];
+                for (uint32_t k = 0; k < 3; k++) {
+                    const uint32_t c = fkey(centre(b, k));
+                    atomicMin(&bmn[k * (kMax / 2) + g.ord], c);
+                    atomicMax(&bmx[k * (kMax / 2) + g.ord], c);
+                }
+            }
+        }
+        __syncthreads();
+        for (uint32_t p = tid; p < np; p += 1024u) {
+            uint64_t kk = ~0ull;
+            if (p < n) {
+                const Seg g = descend(n, p, lev);
+                uint32_t k32 = 0;
+                if (g.hi - g.lo >= 2u) {
+                    float d[3];
+                    for (uint32_t k = 0; k < 3; k++)
+                        d[k] = funkey(bmx[k * (kMax / 2) + g.ord]) - funkey(bmn[k * (kMax / 2) + g.ord]);
+                    const uint32_t dim = d[0] > d[1] ? (d[0] > d[2] ? 0u : 2u) : (d[1] > d[2] ? 1u : 2u);
+                    k32 = fkey(centre(pool[perm[p]], dim));
+                }
+                kk = ((uint64_t)g.lo << 44) | ((uint64_t)k32 << 12) | p;
+            }
+            key[p] = kk;
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= np; k <<= 1)       // bitonic sort, ascending
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = tid; i < np; i += 1024u) {
+                    const uint32_t x = i ^ j;
+                    if (x > i) {
+                        const uint64_t a = key[i], b = key[x];
+                        if ((a > b) == ((i & k) == 0u)) {
+                            key[i] = b;
+                            key[x] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        for (uint32_t p = tid; p < n; p += 1024u) pre[p] = perm[(uint32_t)(key[p] & 0xFFFu)];
+        __syncthreads();
+        for (uint32_t p = tid; p < n; p += 1024u) perm[p] = pre[p];
+        __syncthreads();
+    }
+    // exclusive prefix of the leaves' subtree sizes, in position order
+    {
+        uint32_t loc[4], sum = 0;
+        for (uint32_t r = 0; r < 4; r++) {
+            const uint32_t p = tid * 4u + r;
+            loc[r] = p < n ? pool[perm[p]].size : 0u;
+            sum += loc[r];
+        }
+        uint32_t* part = bmn;   // 1024 partial sums (the sort scratch is free)
+        part[tid] = sum;
+        __syncthreads();
+        for (uint32_t off = 1; off < 1024u; off <<= 1) {
+            const uint32_t v = tid >= off ? part[tid - off] : 0u;
+            __syncthreads();
+            part[tid] += v;
+            __syncthreads();
+        }
+        uint32_t run = part[tid] - sum;
+        for (uint32_t r = 0; r < 4; r++) {
+            const uint32_t p = tid * 4u + r;
+            if (p <= n) pre[p] = run;
+            run += loc[r];
+        }
+        __syncthreads();
+    }
+    // treelet roots: DFS index of each leaf position
+    for (uint32_t p = tid; p < n; p += 1024u) {
+        const Seg g = descend(n, p, 32u);
+        pool[perm[p]].dfs = pre[p] + g.depth + p - g.rights;
+    }
+    // internal nodes: boxes bottom-up by depth (deepest first), then the records
+    for (int dep = (int)L - 1; dep >= 0; dep--) {
+        for (uint32_t m = 1u + tid; m < n; m += 1024u) {
+            const Seg g = node_of(n, m);
+            if ((int)g.depth != dep) continue;
+            float cb[2][6];
+            const uint32_t cl[2] = {g.lo, m}, ch[2] = {m, g.hi};
+            for (int c = 0; c < 2; c++) {
+                if (ch[c] - cl[c] == 1u) {
+                    const BNode& b = pool[perm[cl[c]]];
+                    for (int k = 0; k < 3; k++) {
+                        cb[c][k] = b.mn[k];
+                        cb[c][3 + k] = b.mx[k];
+                    }
+                } else {
+                    const uint32_t cm = cl[c] + (ch[c] - cl[c]) / 2u;
+                    for (int k = 0; k < 6; k++) cb[c][k] = box[(cm - 1u) * 6u + k];
+                }
+            }
+            for (int k = 0; k < 3; k++) {
+                box[(m - 1u) * 6u + k] = rt_minf(cb[0][k], cb[1][k]);
+                box[(m - 1u) * 6u + 3 + k] = rt_maxf(cb[0][3 + k], cb[1][3 + k]);
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t m = 1u + tid; m < n; m += 1024u) {
+        const Seg g = node_of(n, m);
+        const uint32_t dfs = pre[g.lo] + g.depth + g.lo - g.rights;
+        rt_gpu_node r;
+        for (int k = 0; k < 3; k++) {
+            r.min[k] = box[(m - 1u) * 6u + k];
+            r.max[k] = box[(m - 1u) * 6u + 3 + k];
+        }
+        r.offset_ptr = dfs + 1u + (m - g.lo - 1u) + pre[m] - pre[g.lo];   // right child: after the left subtree
+        r.n_prims = 0;
+        up[m - 1u] = r;
+        up_at[m - 1u] = dfs;
+    }
+    if (tid == 0) {   // GpuNode::new(root bbox) filler (hlbvh.rs:518-525)
+        if (n == 1u) {
+            for (int k = 0; k < 3; k++) {
+                root_box[k] = pool[0].mn[k];
+                root_box[3 + k] = pool[0].mx[k];
+            }
+        } else {
+            const uint32_t m = n / 2u;
+            for (int k = 0; k < 6; k++) root_box[k] = box[(m - 1u) * 6u + k];
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_fill_nodes_dev(rt_gpu_node* out, uint32_t n, const float* root_box)
+{
+    rt_gpu_node f;
+    for (int k = 0; k < 3; k++) {
+        f.min[k] = root_box[k];
+        f.max[k] = root_box[3 + k];
+    }
+    f.offset_ptr = 9999;
+    f.n_prims = 9999;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) out[i] = f;
 }
 
 // ------------------------------------------------------------ device-wide exclusive scan
@@ -683,66 +911,31 @@ int build_bvh_device(const float4* pos, const uint4* idx, uint32_t nt, uint32_t 
         hipLaunchKernelGGL(k_bottom_up, dim3(grid), dim3(256), 0, s, ctl, (uint32_t)L, res, pool);
     chk("treelet build");
     (void)hipEventRecord(ev[4], s);
-    // -- upper tree on the host (<= 4096 treelet roots)
+    // -- upper tree on the device (<= 4096 treelet roots, k_upper_tree); the host
+    //    only reads the two counts that size the output (the reference's total_nodes)
     Ctl hc;
     if (e == hipSuccess) e = hipMemcpyAsync(&hc, ctl, sizeof hc, hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    std::vector<BNode> roots(hc.ntreelets);
-    if (e == hipSuccess && hc.ntreelets)
-        e = hipMemcpyAsync(roots.data(), pool, sizeof(BNode) * hc.ntreelets, hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
         if (err.empty()) err = std::string("rt_build_bvh_device: ") + hipGetErrorString(e);
         return RT_E_DEVICE;
     }
-    const auto t_up0 = std::chrono::steady_clock::now();
-    std::vector<float> rb((size_t)hc.ntreelets * 6);
-    for (uint32_t i = 0; i < hc.ntreelets; i++)
-        for (int k = 0; k < 3; k++) {
-            rb[(size_t)i * 6 + k] = roots[i].mn[k];
-            rb[(size_t)i * 6 + 3 + k] = roots[i].mx[k];
-        }
-    std::vector<rthost::UpperNode> up;
-    const uint32_t upper_internal = rthost::bvh_upper_tree(rb, up);
-    const uint32_t total = hc.emits + upper_internal;   // the reference's total_nodes (array length)
-    // DFS offsets: upper internal nodes in place, a treelet root at its subtree's start
-    std::vector<uint32_t> root_dfs(hc.ntreelets, 0);
-    std::vector<rt_gpu_node> up_nodes;
-    std::vector<uint32_t> up_at;
-    uint32_t next = 0;
-    std::vector<uint32_t> entry_dfs(up.size(), 0);
-    // iterative pre-order walk (left subtree before right)
-    std::vector<int32_t> stack{0};
-    while (!stack.empty()) {
-        const int32_t i = stack.back();
-        stack.pop_back();
-        entry_dfs[i] = next;
-        if (up[i].root >= 0) {
-            root_dfs[up[i].root] = next;
-            next += roots[up[i].root].size;
-        } else {
-            next += 1;
-            stack.push_back(up[i].right);
-            stack.push_back(up[i].left);
-        }
-    }
-    for (size_t i = 0; i < up.size(); i++)
-        if (up[i].root < 0) {
-            rt_gpu_node g;
-            for (int k = 0; k < 3; k++) {
-                g.min[k] = up[i].mn[k];
-                g.max[k] = up[i].mx[k];
-            }
-            g.offset_ptr = entry_dfs[up[i].right];
-            g.n_prims = 0;
-            up_nodes.push_back(g);
-            up_at.push_back(entry_dfs[i]);
-        }
-    if (next > total) {
-        err = "rt_build_bvh_device: node count mismatch";
+    if (hc.ntreelets == 0u || hc.ntreelets > upper::kMax) {
+        err = "rt_build_bvh_device: treelet count out of range";
         return RT_E_DEVICE;
     }
-    const auto t_up1 = std::chrono::steady_clock::now();
+    const uint32_t n_up = hc.ntreelets - 1u;            // internal nodes of the upper tree
+    const uint32_t total = hc.emits + n_up;             // the reference's total_nodes (array length)
+    rt_gpu_node* d_up = S.alloc<rt_gpu_node>(std::max(1u, n_up), e);
+    uint32_t* d_upat = S.alloc<uint32_t>(std::max(1u, n_up), e);
+    float* d_rootbox = S.alloc<float>(8, e);
+    if (e != hipSuccess) {
+        err = "rt_build_bvh_device: scratch allocation for the upper tree failed";
+        return RT_E_OOM;
+    }
+    hipLaunchKernelGGL(k_upper_tree, dim3(1), dim3(1024), 0, s, ctl, pool, d_up, d_upat, d_rootbox);
+    chk("upper tree");
+    (void)hipEventRecord(ev[5], s);
     // -- flattening
     out.nnodes = total;
     out.nids = nt;
@@ -751,35 +944,12 @@ int build_bvh_device(const float4* pos, const uint4* idx, uint32_t nt, uint32_t 
         err = "rt_build_bvh_device: output allocation failed";
         return RT_E_OOM;
     }
-    uint32_t* d_rootdfs = S.alloc<uint32_t>(hc.ntreelets, e);
-    rt_gpu_node* d_up = S.alloc<rt_gpu_node>(up_nodes.size(), e);
-    uint32_t* d_upat = S.alloc<uint32_t>(up_at.size(), e);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_rootdfs, root_dfs.data(), root_dfs.size() * 4, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && !up_nodes.empty())
-        e = hipMemcpyAsync(d_up, up_nodes.data(), up_nodes.size() * sizeof(rt_gpu_node), hipMemcpyHostToDevice, s);
-    if (e == hipSuccess && !up_at.empty())
-        e = hipMemcpyAsync(d_upat, up_at.data(), up_at.size() * 4, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-        err = std::string("rt_build_bvh_device: upload of the upper tree: ") + hipGetErrorString(e);
-        return RT_E_DEVICE;
-    }
-    (void)hipEventRecord(ev[5], s);
-    rt_gpu_node filler;   // GpuNode::new(root bbox), hlbvh.rs:518-525
-    const rthost::UpperNode& R = up[0];
-    for (int k = 0; k < 3; k++) {
-        filler.min[k] = R.mn[k];
-        filler.max[k] = R.mx[k];
-    }
-    filler.offset_ptr = 9999;
-    filler.n_prims = 9999;
-    hipLaunchKernelGGL(k_set_dfs, dim3(grid), dim3(256), 0, s, d_rootdfs, hc.ntreelets, pool);
     for (uint32_t L = 0; L < (uint32_t)kLevels; L++)
         hipLaunchKernelGGL(k_top_down, dim3(grid), dim3(256), 0, s, ctl, L, res, pool);
-    hipLaunchKernelGGL(k_fill_nodes, dim3(grid), dim3(256), 0, s, out.nodes, total, filler);
+    hipLaunchKernelGGL(k_fill_nodes_dev, dim3(grid), dim3(256), 0, s, out.nodes, total, d_rootbox);
     hipLaunchKernelGGL(k_write_nodes, dim3(grid), dim3(256), 0, s, ctl, pool, out.nodes);
-    if (!up_nodes.empty())
-        hipLaunchKernelGGL(k_scatter_nodes, dim3(grid), dim3(256), 0, s, d_up, d_upat, (uint32_t)up_nodes.size(),
-                           out.nodes);
+    if (n_up)
+        hipLaunchKernelGGL(k_scatter_nodes, dim3(grid), dim3(256), 0, s, d_up, d_upat, n_up, out.nodes);
     (void)hipMemcpyAsync(out.ids, v0, (size_t)nt * 4, hipMemcpyDeviceToDevice, s);
     chk("flatten");
     (void)hipEventRecord(ev[6], s);
@@ -796,11 +966,11 @@ int build_bvh_device(const float4* pos, const uint4* idx, uint32_t nt, uint32_t 
         times->radix_sort_ms = ms[1];
         times->treelet_init_ms = ms[2];
         times->treelet_build_ms = ms[3];
-        // upper tree: D2H of the roots + host collapse + H2D (wall clock)
+        // upper tree: the count read-back + k_upper_tree (no host work left)
         float up_ms = 0.0f;
         (void)hipEventElapsedTime(&up_ms, ev[4], ev[5]);
         times->upper_tree_ms = up_ms;
-        times->upper_tree_host_ms = std::chrono::duration<double, std::milli>(t_up1 - t_up0).count();
+        times->upper_tree_host_ms = 0.0;
         times->flattening_ms = ms[5];
         times->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
         times->treelets = hc.ntreelets;

@@ -222,3 +222,25 @@ def test_prng_and_math(oracle):
     xs = np.linspace(-1, 1, 2001, dtype=np.float32)
     err = max(abs(L.or_det_acosf(float(x)) - np.arccos(np.float64(x))) for x in xs)
     assert err < 5e-7
+
+
+def test_bvh_closest_hit_agrees_with_brute_force(oracle):
+    """The BVH walk (bvh.wgsl:154-191) finds the brute-force closest hit: the
+    same distance (coplanar ties may pick another triangle), on the teapot with
+    rays from all around it; no ray here reaches the 1000-pop cap."""
+    m = oracle.load_obj(model("teapot.obj"))
+    sc = oracle.SceneRef(m, None, oracle.build_bvh(m, 4))
+    rng = np.random.default_rng(11)
+    hits = 0
+    for _ in range(400):
+        o = rng.uniform([-4, -1, -4], [4, 4, 4]).astype(np.float32)
+        tgt = m.pos[m.idx[rng.integers(0, m.ntris), 0], :3]
+        w = (tgt - o + rng.normal(scale=0.2, size=3)).astype(np.float32)
+        w = (w / np.float32(np.sqrt(np.float32(np.dot(w, w))))).astype(np.float32)
+        h1, t1, d1 = oracle.trace_one(sc, "BVH", o, w, 1e-4, 1e5)
+        h2, t2, d2 = oracle.trace_brute(sc, o, w, 1e-4, 1e5)
+        assert h1 == h2
+        if h1:
+            hits += 1
+            assert d1 == d2 or abs(d1 - d2) <= 1e-6 * d2
+    assert hits > 150
