@@ -557,14 +557,12 @@ __global__ void __launch_bounds__(1024) k_upper_tree(const Ctl* ctl, BNode* pool
         __syncthreads();
         for (uint32_t k = 2; k <= np; k <<= 1)       // bitonic sort, ascending
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t i = tid; i < np; i += 1024u) {
-                    const uint32_t x = i ^ j;
-                    if (x > i) {
-                        const uint64_t a = key[i], b = key[x];
-                        if ((a > b) == ((i & k) == 0u)) {
-                            key[i] = b;
-                            key[x] = a;
-                        }
+                for (uint32_t q = tid; q < np / 2u; q += 1024u) {   // compare-exchange pair q: (i, i + j)
+                    const uint32_t i = ((q & ~(j - 1u)) << 1) | (q & (j - 1u));
+                    const uint64_t a = key[i], b = key[i + j];
+                    if ((a > b) == ((i & k) == 0u)) {
+                        key[i] = b;
+                        key[i + j] = a;
                     }
                 }
                 __syncthreads();
@@ -854,6 +852,9 @@ int build_bvh_device(const float4* pos, const uint4* idx, uint32_t nt, uint32_t 
     BNode* pool = S.alloc<BNode>(pool_cap, e);
     uint32_t* res = S.alloc<uint32_t>(pool_cap, e);
     Ctl* ctl = S.alloc<Ctl>(1, e);
+    rt_gpu_node* d_up = S.alloc<rt_gpu_node>(upper::kMax, e);   // upper-tree records and their DFS slots
+    uint32_t* d_upat = S.alloc<uint32_t>(upper::kMax, e);
+    float* d_rootbox = S.alloc<float>(8, e);
     if (e != hipSuccess) {
         err = std::string("rt_build_bvh_device: scratch allocation: ") + hipGetErrorString(e);
         return e == hipErrorOutOfMemory ? RT_E_OOM : RT_E_DEVICE;
@@ -926,13 +927,6 @@ int build_bvh_device(const float4* pos, const uint4* idx, uint32_t nt, uint32_t 
     }
     const uint32_t n_up = hc.ntreelets - 1u;            // internal nodes of the upper tree
     const uint32_t total = hc.emits + n_up;             // the reference's total_nodes (array length)
-    rt_gpu_node* d_up = S.alloc<rt_gpu_node>(std::max(1u, n_up), e);
-    uint32_t* d_upat = S.alloc<uint32_t>(std::max(1u, n_up), e);
-    float* d_rootbox = S.alloc<float>(8, e);
-    if (e != hipSuccess) {
-        err = "rt_build_bvh_device: scratch allocation for the upper tree failed";
-        return RT_E_OOM;
-    }
     hipLaunchKernelGGL(k_upper_tree, dim3(1), dim3(1024), 0, s, ctl, pool, d_up, d_upat, d_rootbox);
     chk("upper tree");
     (void)hipEventRecord(ev[5], s);
