@@ -2,7 +2,7 @@
 # One GPU-box session: the GPU test suite, then measurement steps.  A test
 # failure (pytest rc 1) is reported and the measurements still run; any other
 # failure (fault, abort, time limit) ends the session.
-# usage: tools/gpu_session.sh <tag> [step ...]   steps: tests | build | c3 | c5 | c4 | c2 | bvh3
+# usage: tools/gpu_session.sh <tag> [step ...]   steps: tests | build | c3 | c5 | c4 | c2 | bvh3 | probe
 set -u
 TAG=$1; shift
 export TMPDIR=/tmp
@@ -20,6 +20,7 @@ for step in "$@"; do
     c2) bash tools/measure.sh $TAG/c2 --config 2 || exit 1 ;;
     c4) bash tools/measure.sh $TAG/c4 --config 4 --spp 64 || exit 1 ;;
     c5) bash tools/measure.sh $TAG/c5 --config 5 --spp 64 --shade-threshold 32 || exit 1 ;;
+    probe) timeout -k 10 120 ./tools/probes/issue_probe > $OUT/issue_probe.txt 2>&1; rc=$?; cat $OUT/issue_probe.txt; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
