@@ -2,7 +2,10 @@
 cross-compiles gfx950 here).  A spill reload inside k_path's traversal trip
 loop cost 18 % of the config-3 frame when an unrelated shading change moved
 the allocator's choices.  The default instantiations'
-trip loops may hold only the spill stores of the accept path they hold today."""
+trip loops may hold only the spill stores of the accept path they hold today,
+and the whole kernel's spill footprint (scratch bytes per lane, spill
+instructions) may not grow: the shading-phase spills are most of the kernel's
+HBM traffic ("HBM traffic")."""
 import os
 import subprocess
 import sys
@@ -30,6 +33,33 @@ def device_asm(tmp_path_factory):
         pytest.skip("hipcc not available")
     subprocess.run(cmd, check=True, capture_output=True, timeout=600)
     return str(out)
+
+
+# kernel -> (scratch bytes per lane, scratch instructions in the whole kernel), today's values
+WHOLE_BUDGET = {
+    "k_pathILi4ELi0ELb0": (176, 99),    # W9E1, BSP
+    "k_pathILi4ELi1ELb0": (168, 97),    # W9E1, BVH
+}
+
+
+def kernel_spills(path, ksub):
+    import re
+    s = open(path).read()
+    name = next(l.split(":")[0] for l in s.splitlines() if re.match(r"^_Z\S*:", l) and ksub in l)
+    i = s.index(name + ":")
+    body = s[i:s.index(".Lfunc_end", i)]
+    k = s.index(".amdhsa_kernel " + name)
+    meta = s[k:s.index(".end_amdhsa_kernel", k)]
+    scratch = int(re.search(r"\.amdhsa_private_segment_fixed_size (\d+)", meta).group(1))
+    return scratch, len(re.findall(r"\bscratch_(?:load|store)", body))
+
+
+@pytest.mark.parametrize("kernel", sorted(WHOLE_BUDGET))
+def test_whole_kernel_spills_within_budget(device_asm, kernel):
+    scratch, ops = kernel_spills(device_asm, kernel)
+    b_scratch, b_ops = WHOLE_BUDGET[kernel]
+    assert scratch <= b_scratch, f"{kernel}: {scratch} B of scratch per lane (budget {b_scratch})"
+    assert ops <= b_ops, f"{kernel}: {ops} spill instructions (budget {b_ops})"
 
 
 @pytest.mark.parametrize("kernel", sorted(BUDGET))

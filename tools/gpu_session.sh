@@ -20,7 +20,7 @@ for step in "$@"; do
     c2) bash tools/measure.sh $TAG/c2 --config 2 || exit 1 ;;
     c4) bash tools/measure.sh $TAG/c4 --config 4 --spp 64 || exit 1 ;;
     c5) bash tools/measure.sh $TAG/c5 --config 5 --spp 64 --shade-threshold 32 || exit 1 ;;
-    probe) timeout -k 10 120 ./tools/probes/issue_probe > $OUT/issue_probe.txt 2>&1; rc=$?; cat $OUT/issue_probe.txt; [ $rc -eq 0 ] || exit $rc ;;
+    probe) timeout -k 10 40 ./tools/probes/issue_probe > $OUT/issue_probe.txt 2>&1; rc=$?; cat $OUT/issue_probe.txt; [ $rc -eq 0 ] || exit $rc ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -14,7 +14,9 @@ __global__ void __launch_bounds__(256) k_probe(unsigned* out, int iters)
         if (KIND == 0 || KIND == 2)
             asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1\n\t"
                          "s_add_u32 %0, %0, 1\n\ts_add_u32 %1, %1, 1\n\ts_add_u32 %2, %2, 1\n\ts_add_u32 %3, %3, 1"
-                         : "+s"(sa), "+s"(sb), "+s"(sc), "+s"(sd));
+                         : "+s"(sa), "+s"(sb), "+s"(sc), "+s"(sd)
+                         :
+                         : "scc");
         if (KIND == 1 || KIND == 2)
             asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1\n\t"
                          "v_add_u32 %0, %0, 1\n\tv_add_u32 %1, %1, 1\n\tv_add_u32 %2, %2, 1\n\tv_add_u32 %3, %3, 1"
