@@ -505,10 +505,11 @@ __global__ void __launch_bounds__(1024) k_upper_tree(const Ctl* ctl, BNode* pool
 {
     using namespace upper;
     __shared__ uint32_t perm[kMax], pre[kMax + 1];
-    // sort phase: keys + per-segment centroid bounds; output phase: node boxes
-    __shared__ __attribute__((aligned(16))) uint8_t pool_lds[kMax * 24];
-    uint64_t* key = reinterpret_cast<uint64_t*>(pool_lds);                     // [kMax]
-    uint32_t* bmn = reinterpret_cast<uint32_t*>(pool_lds + kMax * 8);          // [3][kMax/2]
+    // sort phase: keys (segments padded to a power of two) + per-segment
+    // centroid bounds; output phase: node boxes
+    __shared__ __attribute__((aligned(16))) uint8_t pool_lds[2 * kMax * 8 + 6 * (kMax / 2) * 4];
+    uint64_t* key = reinterpret_cast<uint64_t*>(pool_lds);                     // [2 kMax]
+    uint32_t* bmn = reinterpret_cast<uint32_t*>(pool_lds + 2 * kMax * 8);      // [3][kMax/2]
     uint32_t* bmx = bmn + 3 * (kMax / 2);
     float* box = reinterpret_cast<float*>(pool_lds);                           // [kMax-1][6]
     const uint32_t tid = threadIdx.x, n = ctl->ntreelets;
@@ -538,36 +539,45 @@ __global__ void __launch_bounds__(1024) k_upper_tree(const Ctl* ctl, BNode* pool
             }
         }
         __syncthreads();
-        for (uint32_t p = tid; p < np; p += 1024u) {
-            uint64_t kk = ~0ull;
-            if (p < n) {
-                const Seg g = descend(n, p, lev);
-                uint32_t k32 = 0;
-                if (g.hi - g.lo >= 2u) {
-                    float d[3];
-                    for (uint32_t k = 0; k < 3; k++)
-                        d[k] = funkey(bmx[k * (kMax / 2) + g.ord]) - funkey(bmn[k * (kMax / 2) + g.ord]);
-                    const uint32_t dim = d[0] > d[1] ? (d[0] > d[2] ? 0u : 2u) : (d[1] > d[2] ? 1u : 2u);
-                    k32 = fkey(centre(pool[perm[p]], dim));
-                }
-                kk = ((uint64_t)g.lo << 44) | ((uint64_t)k32 << 12) | p;
+        // every segment of this level in its own block of B (a power of two >= the
+        // largest segment, ceil(n / 2^lev)) slots: B << lev <= 2 np keys, sorted block
+        // by block -- log2(B) stages instead of log2(np)
+        uint32_t B = 1;
+        while (B < ((n + (1u << lev) - 1u) >> lev)) B <<= 1;
+        const uint32_t tot = B << lev;
+        for (uint32_t i = tid; i < tot; i += 1024u) key[i] = ~0ull;
+        __syncthreads();
+        for (uint32_t p = tid; p < n; p += 1024u) {
+            const Seg g = descend(n, p, lev);
+            uint32_t k32 = 0;
+            if (g.hi - g.lo >= 2u) {
+                float d[3];
+                for (uint32_t k = 0; k < 3; k++)
+                    d[k] = funkey(bmx[k * (kMax / 2) + g.ord]) - funkey(bmn[k * (kMax / 2) + g.ord]);
+                const uint32_t dim = d[0] > d[1] ? (d[0] > d[2] ? 0u : 2u) : (d[1] > d[2] ? 1u : 2u);
+                k32 = fkey(centre(pool[perm[p]], dim));
             }
-            key[p] = kk;
+            // a single-member segment that stopped above this level keeps its block at
+            // its ordinal scaled to this depth (no real segment lives under it)
+            key[(g.ord << (lev - g.depth)) * B + (p - g.lo)] = ((uint64_t)k32 << 12) | p;   // ties: the order above
         }
         __syncthreads();
-        for (uint32_t k = 2; k <= np; k <<= 1)       // bitonic sort, ascending
+        for (uint32_t k = 2; k <= B; k <<= 1)        // bitonic sort of each block, ascending
             for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                for (uint32_t q = tid; q < np / 2u; q += 1024u) {   // compare-exchange pair q: (i, i + j)
+                for (uint32_t q = tid; q < tot / 2u; q += 1024u) {   // compare-exchange pair q: (i, i + j)
                     const uint32_t i = ((q & ~(j - 1u)) << 1) | (q & (j - 1u));
                     const uint64_t a = key[i], b = key[i + j];
-                    if ((a > b) == ((i & k) == 0u)) {
+                    if ((a > b) == ((k == B) | ((i & k) == 0u))) {
                         key[i] = b;
                         key[i + j] = a;
                     }
                 }
                 __syncthreads();
             }
-        for (uint32_t p = tid; p < n; p += 1024u) pre[p] = perm[(uint32_t)(key[p] & 0xFFFu)];
+        for (uint32_t p = tid; p < n; p += 1024u) {
+            const Seg g = descend(n, p, lev);
+            pre[p] = perm[(uint32_t)(key[(g.ord << (lev - g.depth)) * B + (p - g.lo)] & 0xFFFu)];
+        }
         __syncthreads();
         for (uint32_t p = tid; p < n; p += 1024u) perm[p] = pre[p];
         __syncthreads();

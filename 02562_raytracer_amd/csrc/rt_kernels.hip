@@ -811,6 +811,13 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 #ifndef RT_BVH_WAVES_PER_EU
 #define RT_BVH_WAVES_PER_EU 7
 #endif
+// W7E3 (config 2): its area-light shading keeps more state than W9E1's.  At 8
+// waves/SIMD (64 VGPRs) it spilled 272 B per lane and moved 103 GB per config-2
+// launch through L2 for 1 GB of sample records; at 5 (96 VGPRs) 76 B and 10 GB,
+// and the frame is 3.5 % faster: 4528 vs 4375 Mrays/s (profiles/r02/ab_w7e3_waves.txt)
+#ifndef RT_W7E3_WAVES_PER_EU
+#define RT_W7E3_WAVES_PER_EU 5
+#endif
 #ifndef RT_PATH_WAVES_PER_EU
 #define RT_PATH_WAVES_PER_EU 8
 #endif
@@ -983,7 +990,8 @@ constexpr int MODE_W9E1_TRANSPARENT = 100 + RT_MODE_W9E1;
 
 template <int MODE, int TRAV, bool COUNT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
-    TRAV == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : RT_PATH_WAVES_PER_EU, 8)))
+    TRAV == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : MODE == RT_MODE_W7E3 ? RT_W7E3_WAVES_PER_EU : RT_PATH_WAVES_PER_EU,
+    8)))
 k_path(DevScene S, DevLaunch L)
 {
     extern __shared__ uint32_t lds_stack[];   // [level][thread], 4 B entries
@@ -2081,7 +2089,9 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
     // would only add blocks that start after the queue ran dry
     const int lds_waves = 4 * (int)((160u * 1024u) / (lds ? lds : 1));
     // and by the register budget k_path is fitted to (waves per SIMD x 4 SIMDs)
-    const int reg_waves = 4 * (trav == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : RT_PATH_WAVES_PER_EU);
+    const int reg_waves = 4 * (trav == RT_TRAVERSE_BVH    ? RT_BVH_WAVES_PER_EU
+                               : mode == RT_MODE_W7E3 ? RT_W7E3_WAVES_PER_EU
+                                                      : RT_PATH_WAVES_PER_EU);
     const int grid = grid_for(num_cus, std::min(std::min(waves_per_cu > 0 ? waves_per_cu : 16, reg_waves),
                                                 std::max(4, lds_waves)));
     if (mode == RT_MODE_W1E6) {

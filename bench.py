@@ -35,6 +35,10 @@ L2_PEAK_GBS = 34500.0   # aggregate L2 (8 XCDs x 4 MiB), MI355X_MICROARCH.md "L2
 NUM_CUS, SIMDS_PER_CU, MAX_CLOCK_GHZ = 256, 4, 2.4
 VALU_PEAK_GINSTS = NUM_CUS * SIMDS_PER_CU * MAX_CLOCK_GHZ / 2.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+# SALU issue: the scalar ALU is one per-CU resource; tools/probes/issue_probe.hip
+# measured it saturating at 0.758 wave-instructions per shader cycle per CU
+# (profiles/r02/issue_probe.txt; the microarchitecture guide gives no figure)
+SALU_PEAK_GINSTS = NUM_CUS * 0.758 * MAX_CLOCK_GHZ
 METRIC = "Mrays/sec primary+shadow at 1920x1080; achieved HBM GB/s vs peak"
 
 
@@ -127,12 +131,18 @@ def roofline(key, kern_ms, alg_bytes, config, kernel):
                 "frac": round(hbm_gbs / HBM_PEAK_GBS, 4)}
     r["valu_issue"] = {"achieved": round(valu, 1), "peak": round(VALU_PEAK_GINSTS, 1),
                        "unit": "G wave64 VALU instr/s", "frac": round(valu / VALU_PEAK_GINSTS, 4)}
+    if "salu_insts_per_launch" in pmc:
+        salu = pmc["salu_insts_per_launch"] / s / 1e9
+        r["salu_issue"] = {"achieved": round(salu, 1), "peak": round(SALU_PEAK_GINSTS, 1),
+                           "unit": "G wave SALU instr/s", "frac": round(salu / SALU_PEAK_GINSTS, 4),
+                           "peak_source": "measured ceiling, tools/probes/issue_probe.hip"}
     r["pmc"] = {k: pmc[k] for k in ("source", "kernel_ms_profiled", "l2_hit_rate", "valu_lane_util", "wait_frac",
                                     "write_bytes_per_launch", "fetch_bytes_per_launch") if k in pmc}
     prim = r["hbm"] if config == 5 else r["valu_issue"]
     r.update({"bound": "hbm" if config == 5 else "valu-issue", "achieved": prim["achieved"], "peak": prim["peak"],
               "unit": prim["unit"], "frac": prim["frac"]})
-    if max(r["hbm"]["frac"], r["valu_issue"]["frac"]) > 1.0:   # a summary of another kernel build
+    if max(r["hbm"]["frac"], r["valu_issue"]["frac"], r.get("salu_issue", {}).get("frac", 0.0)) > 1.0:
+        # a summary of another kernel build
         r.update({"bound": "unmeasured", "frac": None, "note": f"PMC summary for {key} does not match this kernel"})
     return r
 

@@ -76,6 +76,8 @@ if __name__ == "__main__":
                "fetch_bytes_per_launch": int(2.0 * c["FETCH_SIZE"] * 1024.0),
                "write_bytes_per_launch": int(c["WRITE_SIZE"] * 1024.0),
                "valu_insts_per_launch": int(c["SQ_INSTS_VALU"])}
+        if "SQ_INSTS_SALU" in c:
+            ent["salu_insts_per_launch"] = int(c["SQ_INSTS_SALU"])
         for k in ("l2_hit_rate", "valu_lane_util", "wait_frac", "salu_per_valu", "l1_hit_rate"):
             if k in d:
                 ent[k] = round(d[k], 4)
