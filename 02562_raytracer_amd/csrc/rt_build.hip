@@ -527,16 +527,26 @@ __global__ void __launch_bounds__(1024) k_upper_tree(const Ctl* ctl, BNode* pool
             bmx[i] = 0u;
         }
         __syncthreads();
-        for (uint32_t p = tid; p < n; p += 1024u) {   // centroid bounds (Bbox::include_vertex)
-            const Seg g = descend(n, p, lev);
-            if (g.hi - g.lo >= 2u) {
+        // this thread's positions p = tid + 1024 r: their centroids, loaded together
+        // (one round of global loads per level)
+        float cc[4][3];
+        for (uint32_t r = 0; r < 4; r++) {
+            const uint32_t p = tid + 1024u * r;
+            if (p < n) {
                 const BNode& b = pool[perm[p]];
+                for (uint32_t k = 0; k < 3; k++) cc[r][k] = centre(b, k);
+            }
+        }
+        for (uint32_t r = 0; r < 4; r++) {   // centroid bounds (Bbox::include_vertex)
+            const uint32_t p = tid + 1024u * r;
+            if (p >= n) break;
+            const Seg g = descend(n, p, lev);
+            if (g.hi - g.lo >= 2u)
                 for (uint32_t k = 0; k < 3; k++) {
-                    const uint32_t c = fkey(centre(b, k));
+                    const uint32_t c = fkey(cc[r][k]);
                     atomicMin(&bmn[k * (kMax / 2) + g.ord], c);
                     atomicMax(&bmx[k * (kMax / 2) + g.ord], c);
                 }
-            }
         }
         __syncthreads();
         // every segment of this level in its own block of B (a power of two >= the
@@ -547,7 +557,9 @@ __global__ void __launch_bounds__(1024) k_upper_tree(const Ctl* ctl, BNode* pool
         const uint32_t tot = B << lev;
         for (uint32_t i = tid; i < tot; i += 1024u) key[i] = ~0ull;
         __syncthreads();
-        for (uint32_t p = tid; p < n; p += 1024u) {
+        for (uint32_t r = 0; r < 4; r++) {
+            const uint32_t p = tid + 1024u * r;
+            if (p >= n) break;
             const Seg g = descend(n, p, lev);
             uint32_t k32 = 0;
             if (g.hi - g.lo >= 2u) {
@@ -555,7 +567,7 @@ __global__ void __launch_bounds__(1024) k_upper_tree(const Ctl* ctl, BNode* pool
                 for (uint32_t k = 0; k < 3; k++)
                     d[k] = funkey(bmx[k * (kMax / 2) + g.ord]) - funkey(bmn[k * (kMax / 2) + g.ord]);
                 const uint32_t dim = d[0] > d[1] ? (d[0] > d[2] ? 0u : 2u) : (d[1] > d[2] ? 1u : 2u);
-                k32 = fkey(centre(pool[perm[p]], dim));
+                k32 = fkey(dim == 0u ? cc[r][0] : dim == 1u ? cc[r][1] : cc[r][2]);
             }
             // a single-member segment that stopped above this level keeps its block at
             // its ordinal scaled to this depth (no real segment lives under it)
