@@ -32,7 +32,6 @@ RT_OPT_SAMPLE_CHUNK = 4
 RT_OPT_SAMPLE_BUDGET_MB = 5
 RT_OPT_UNIT_ORDER = 6
 RT_OPT_KERNEL_TIMING = 7
-RT_OPT_MIN_HALF_LANES = 8
 
 MODES = {"W1E6": RT_MODE_W1E6, "W6E1": RT_MODE_W6E1, "PROJECT": RT_MODE_PROJECT, "W7E3": RT_MODE_W7E3,
          "W9E1": RT_MODE_W9E1, "W8E1": RT_MODE_W8E1, "W8E2": RT_MODE_W8E2, "W8E3": RT_MODE_W8E3,

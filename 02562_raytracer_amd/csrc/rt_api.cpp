@@ -62,7 +62,6 @@ struct rt_ctx {
     int num_cus = 256;
     int waves_per_cu = 32;   // 8 waves per SIMD: the k_path register budget (RT_PATH_WAVES_PER_EU)
     int shade_threshold = -1;   // -1: per walk (BSP 8, BVH 4); pixel-major units refill together (coherent samples)
-    uint32_t min_half_lanes = 0;        // k_path trip-half postponement (0: off)
     uint32_t sample_chunk = 1;          // iterations per k_path work unit
     uint32_t unit_order = 1;            // 0: chunk-major, 1: pixel-major
     uint64_t sample_budget_mb = 16384;  // per-sample scratch (one pass at 1080p x 256 spp needs 8.1 GiB)
@@ -270,10 +269,6 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
         return RT_OK;
     case RT_OPT_KERNEL_TIMING:
         c->ktiming = value != 0;
-        return RT_OK;
-    case RT_OPT_MIN_HALF_LANES:
-        if (value < 0 || value > 64) return fail(c, RT_E_INVALID, "min half lanes must be in [0,64]");
-        c->min_half_lanes = (uint32_t)value;
         return RT_OK;
     case RT_OPT_UNIT_ORDER:
         if (value < 0 || value > 1) return fail(c, RT_E_INVALID, "unit order must be 0 or 1");
@@ -837,7 +832,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // default shading threshold per walk (BSP sweep 8 best;
     // BVH 2-4 best, 4695 vs 4604 Mrays/s at 8)
     L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold : trav == RT_TRAVERSE_BVH ? 4 : 8);
-    L.min_half_lanes = c->min_half_lanes;
+    L.reserved0 = 0;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
     if (L.nwork == 0 || (L.spp == 0 && (path || direct_prog))) {

@@ -56,7 +56,7 @@ struct DevLaunch {
     uint32_t nwork;               // work items (tiles) in this launch
     uint32_t first_iter, spp;     // this pass: iterations first_iter .. first_iter+spp-1
     uint32_t shade_threshold;     // k_path: shade when <= this many lanes still trace
-    uint32_t min_half_lanes;      // k_path: postpone a trip half (walk / test) with fewer lanes (0: off)
+    uint32_t reserved0;           // (was the retired trip-half postponement; kept for the argument layout)
     // k_path work units: (chunk of `chunk` iterations, pixel slot), chunk-major;
     // per-iteration radiance + primary id go to samples[(it - first_iter) * stride + out]
     // and k_fold applies the progressive average in order (w7e3.wgsl:261-271)

@@ -1033,7 +1033,6 @@ k_path(DevScene S, DevLaunch L)
     const uint32_t pslots = L.nwork * 64u;            // pixel slots
     const uint32_t nslots = pslots * L.nchunks;       // work units (host keeps this < 2^31)
     const uint32_t T = L.shade_threshold;
-    const uint32_t KH = L.min_half_lanes;
     const f3 env = V(L.env[0], L.env[1], L.env[2]);
     Counters cnt;
 #pragma unroll
@@ -1099,17 +1098,7 @@ k_path(DevScene S, DevLaunch L)
                     cnt.v[C_LEAF_TRIPS] += lm != 0;
                 }
             }
-            bool go = st == ST_TRACE;
-            if (KH > 0u) {
-                // postpone the minority half of a divergent trip: lanes inside a
-                // leaf (triangle test) and walking lanes (node steps) run the two
-                // halves of bsp_step/bvh_step; a half with fewer than KH lanes
-                // waits while the other half has at least KH
-                const bool leafst = tr.leaf_k != tr.leaf_end;
-                const uint32_t nl = (uint32_t)__popcll(__ballot(go && leafst));
-                const uint32_t nn = (uint32_t)__popcll(__ballot(go && !leafst));
-                go = go && (leafst ? (nl >= KH || nn < KH) : (nn >= KH || nl < KH));
-            }
+            const bool go = st == ST_TRACE;
             if (go) {
                 if (trav_step<TRAV, COUNT, W9E3>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }

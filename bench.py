@@ -174,7 +174,6 @@ def main():
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)
-    ap.add_argument("--min-half-lanes", type=int, default=None)
     ap.add_argument("--dump-frame", default=None,
                     help="rank 0 saves the last step's assembled frame (accum + ids) to this .npz")
     args = ap.parse_args()
@@ -225,8 +224,6 @@ def main():
         ctx.set_option(rt._ffi.RT_OPT_SAMPLE_CHUNK, args.sample_chunk)
     if args.unit_order is not None:
         ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, args.unit_order)
-    if args.min_half_lanes is not None:
-        ctx.set_option(rt._ffi.RT_OPT_MIN_HALF_LANES, args.min_half_lanes)
     ctx.upload_mesh(mesh)
     if trav == "BSP":
         accel = mesh.bsp_tree()

@@ -165,7 +165,8 @@ typedef struct rt_ray_counts {
 #define RT_OPT_SAMPLE_BUDGET_MB 5 /* W7E3/W9E1: device scratch for per-sample results, MiB (default 16384);
                                      a render whose spp x pixels x 16 B exceed it runs in several passes */
 #define RT_OPT_KERNEL_TIMING   7  /* 0/1: record HIP events around every traversal-kernel launch */
-#define RT_OPT_MIN_HALF_LANES  8  /* W7E3/W9E1: a trip half (node walk / triangle test) with fewer lanes waits (default 0: off) */
+/* option 8 is retired (trip-half postponement: slower on every BASELINE workload, and its
+   per-trip test cost 1.7-4.4 % even when off, profiles/r02/sweep_KH_c5.txt, ab_nokh.txt) */
 #define RT_OPT_UNIT_ORDER      6  /* W7E3/W9E1 work-unit order: 0 chunk-major, 1 pixel-major (default) */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */

@@ -37,7 +37,7 @@ def device_asm(tmp_path_factory):
 
 # kernel -> (scratch bytes per lane, scratch instructions in the whole kernel), today's values
 WHOLE_BUDGET = {
-    "k_pathILi4ELi0ELb0": (176, 99),    # W9E1, BSP
+    "k_pathILi4ELi0ELb0": (180, 101),   # W9E1, BSP
     "k_pathILi4ELi1ELb0": (168, 97),    # W9E1, BVH
 }
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Runtime-knob sweep of one workload: tools/sweep_knobs.sh <out> "<bench opts>" "<knobs 1>" "<knobs 2>" ...
-# e.g. tools/sweep_knobs.sh o.txt "--config 5 --spp 16" "--shade-threshold 32" "--shade-threshold 32 --min-half-lanes 8"
+# e.g. tools/sweep_knobs.sh o.txt "--config 5 --spp 16" "--shade-threshold 32" "--shade-threshold 24"
 mkdir -p "$(dirname "$1")"; OUT=$1; OPTS=$2; shift 2
 for k in "$@"; do
   echo "== $k $OPTS" >> $OUT
