@@ -818,6 +818,12 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 #ifndef RT_W7E3_WAVES_PER_EU
 #define RT_W7E3_WAVES_PER_EU 5
 #endif
+// traversal steps per shading-threshold check in k_path's trip loop
+// (profiles/r02/ab_tpc2.txt: 2 vs 1 = config 3 +1.4%, BVH +2.6%, config 2 +0.6%;
+// ab_tpc34.txt: 4 vs 2 = config 3 +1.9%, BVH +1.0%, 3 vs 2 config 2 +0.4%)
+#ifndef RT_TRIPS_PER_CHECK
+#define RT_TRIPS_PER_CHECK 4
+#endif
 #ifndef RT_PATH_WAVES_PER_EU
 #define RT_PATH_WAVES_PER_EU 8
 #endif
@@ -1101,6 +1107,15 @@ k_path(DevScene S, DevLaunch L)
             const bool go = st == ST_TRACE;
             if (go) {
                 if (trav_step<TRAV, COUNT, W9E3>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+            }
+            // further steps before the next check: the check (two ballots, a
+            // popcount, the compares) is SALU work, and the SALU is a per-CU
+            // limit here; the counting build checks every trip
+#pragma unroll
+            for (int k = 1; k < (COUNT ? 1 : RT_TRIPS_PER_CHECK); ++k) {
+                if (st == ST_TRACE) {
+                    if (trav_step<TRAV, COUNT, W9E3>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                }
             }
         }
         if (COUNT) {

@@ -17,8 +17,11 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 
 # kernel -> allowed scratch instructions in its trip loop (today's values)
 BUDGET = {
-    "k_pathILi4ELi0ELb0": 2,   # W9E1, BSP: the bench kernel (two stores on a triangle accept)
-    "k_pathILi4ELi1ELb0": 6,   # W9E1, BVH (two pops per trip)
+    # W9E1, BSP: the bench kernel; over the four traversal steps of a trip
+    # (RT_TRIPS_PER_CHECK) stores on a triangle accept and reloads on the rare
+    # exact-division path of the fast reject
+    "k_pathILi4ELi0ELb0": 12,
+    "k_pathILi4ELi1ELb0": 0,   # W9E1, BVH
 }
 
 
@@ -27,6 +30,7 @@ def device_asm(tmp_path_factory):
     out = tmp_path_factory.mktemp("isa") / "rt_kernels.s"
     cmd = ["/opt/rocm/bin/hipcc", "-std=c++17", "-O3", "--offload-arch=gfx950", "-ffp-contract=off",
            "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt", "-Wno-bitwise-instead-of-logical",
+           "-fno-slp-vectorize",   # as the Makefile builds rt_kernels.o
            "-x", "hip", "--cuda-device-only", "-S", os.path.join(ROOT, "02562_raytracer_amd", "csrc", "rt_kernels.hip"),
            "-o", str(out)]
     if not os.path.exists(cmd[0]):
@@ -37,8 +41,9 @@ def device_asm(tmp_path_factory):
 
 # kernel -> (scratch bytes per lane, scratch instructions in the whole kernel), today's values
 WHOLE_BUDGET = {
-    "k_pathILi4ELi0ELb0": (180, 101),   # W9E1, BSP
-    "k_pathILi4ELi1ELb0": (168, 97),    # W9E1, BVH
+    "k_pathILi4ELi0ELb0": (148, 137),   # W9E1, BSP
+    "k_pathILi4ELi1ELb0": (116, 90),    # W9E1, BVH
+    "k_pathILi3ELi0ELb0": (8, 2),       # W7E3, BSP at 5 waves/SIMD
 }
 
 
