@@ -806,10 +806,11 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 #ifndef RT_ENV_TEX
 #define RT_ENV_TEX 1
 #endif
-// BVH instantiations: 7 waves/SIMD (72 VGPRs) -- measured 3007 Mrays/s vs
-// 2712 at 8 and 2946 at 6 (256 spp, bunny stand-in)
+// BVH instantiations: 8 waves/SIMD (64 VGPRs).  Round 1 measured 7 best
+// (3007 Mrays/s vs 2712 at 8); with the SLP-free build and four steps per
+// check 8 wins: 5792 vs 5667 (7) and 5511 (6) (profiles/r02/ab_waves2.txt)
 #ifndef RT_BVH_WAVES_PER_EU
-#define RT_BVH_WAVES_PER_EU 7
+#define RT_BVH_WAVES_PER_EU 8
 #endif
 // W7E3 (config 2): its area-light shading keeps more state than W9E1's.  At 8
 // waves/SIMD (64 VGPRs) it spilled 272 B per lane and moved 103 GB per config-2

@@ -21,7 +21,7 @@ BUDGET = {
     # (RT_TRIPS_PER_CHECK) stores on a triangle accept and reloads on the rare
     # exact-division path of the fast reject
     "k_pathILi4ELi0ELb0": 12,
-    "k_pathILi4ELi1ELb0": 0,   # W9E1, BVH
+    "k_pathILi4ELi1ELb0": 4,   # W9E1, BVH at 8 waves/SIMD
 }
 
 
@@ -42,7 +42,7 @@ def device_asm(tmp_path_factory):
 # kernel -> (scratch bytes per lane, scratch instructions in the whole kernel), today's values
 WHOLE_BUDGET = {
     "k_pathILi4ELi0ELb0": (148, 137),   # W9E1, BSP
-    "k_pathILi4ELi1ELb0": (116, 90),    # W9E1, BVH
+    "k_pathILi4ELi1ELb0": (152, 116),   # W9E1, BVH
     "k_pathILi3ELi0ELb0": (8, 2),       # W7E3, BSP at 5 waves/SIMD
 }
 
