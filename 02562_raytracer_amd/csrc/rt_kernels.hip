@@ -354,6 +354,9 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 // A walk that reaches a leaf starts its triangle range (tested from the next
 // trip on); an empty leaf, or a leaf tested without a hit, pops.  Leaf ranges
 // (leaf_k, leaf_end, hit_k) are byte offsets of records in that buffer.
+#ifndef RT_LEAF_TESTS
+#define RT_LEAF_TESTS 1   // triangle tests per leaf trip of the BSP walk (1 or 2)
+#endif
 template <bool COUNT, bool CULL = false>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
@@ -392,6 +395,28 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             t.gamma = gamma;
         }
         t.leaf_k += 48u;
+#if RT_LEAF_TESTS > 1
+        // a second test in the same trip: the next record's first 16 B are
+        // q3 (records are 48 B apart), its other 32 B one more round trip
+        if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
+            const v4u p1 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 16u, 0, 0);
+            const v4u p2 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
+            if (COUNT) {
+                c.v[C_IDS]++;
+                c.v[C_TESTS]++;
+            }
+            if (tri_math<true, COUNT, CULL>(as_f4(q3), as_f4(p1), as_f4(p2), o, d, t.tmin, t.tmax, dist, beta, gamma,
+                                             &c)) {
+                if (COUNT) c.v[C_ACCEPTS]++;
+                t.tmax = dist;
+                t.found = true;
+                t.hit_k = t.leaf_k;
+                t.beta = beta;
+                t.gamma = gamma;
+            }
+            t.leaf_k += 48u;
+        }
+#endif
         const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
         done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
         pop = leaf_done & !t.found;
@@ -821,9 +846,13 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 #endif
 // traversal steps per shading-threshold check in k_path's trip loop
 // (profiles/r02/ab_tpc2.txt: 2 vs 1 = config 3 +1.4%, BVH +2.6%, config 2 +0.6%;
-// ab_tpc34.txt: 4 vs 2 = config 3 +1.9%, BVH +1.0%, 3 vs 2 config 2 +0.4%)
+// ab_tpc34.txt: 4 vs 2 = config 3 +1.9%, BVH +1.0%, 3 vs 2 config 2 +0.4%;
+// ab_tpc8.txt: 8 vs 4 = config 3 +1.2%, config 4 +1.1%, BVH -1.2%)
 #ifndef RT_TRIPS_PER_CHECK
-#define RT_TRIPS_PER_CHECK 4
+#define RT_TRIPS_PER_CHECK 8
+#endif
+#ifndef RT_BVH_TRIPS_PER_CHECK
+#define RT_BVH_TRIPS_PER_CHECK 4
 #endif
 #ifndef RT_PATH_WAVES_PER_EU
 #define RT_PATH_WAVES_PER_EU 8
@@ -1113,7 +1142,7 @@ k_path(DevScene S, DevLaunch L)
             // popcount, the compares) is SALU work, and the SALU is a per-CU
             // limit here; the counting build checks every trip
 #pragma unroll
-            for (int k = 1; k < (COUNT ? 1 : RT_TRIPS_PER_CHECK); ++k) {
+            for (int k = 1; k < (COUNT ? 1 : TRAV == RT_TRAVERSE_BVH ? RT_BVH_TRIPS_PER_CHECK : RT_TRIPS_PER_CHECK); ++k) {
                 if (st == ST_TRACE) {
                     if (trav_step<TRAV, COUNT, W9E3>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
                 }
