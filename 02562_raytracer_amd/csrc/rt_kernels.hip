@@ -354,9 +354,44 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 // A walk that reaches a leaf starts its triangle range (tested from the next
 // trip on); an empty leaf, or a leaf tested without a hit, pops.  Leaf ranges
 // (leaf_k, leaf_end, hit_k) are byte offsets of records in that buffer.
+// A second triangle test of a leaf in the same trip (BSP walk).  A leaf
+// lane's trip loads 64 B at its record: the 48-B record it tests and the
+// first 16 B of the next one (`nx`; records of a leaf are 48 B apart).  The
+// next record is tested in order, after the first one's accept has narrowed
+// tmax, exactly as one test per trip would; its other 32 B cost one more
+// round trip.  A walk that stops at its first hit (anyhit) stops here too.
+// Two tests per trip take the per-trip costs (the check, the walking half of
+// the wave, the pop) off the leaf work: config 3 +2.9 %, config 4 +12 %,
+// config 5 (32-triangle leaves) +20 % (profiles/r02/ab_lt2.txt); three or more
+// per trip, or the same for the BVH walk (leaves of at most 4), were slower
+// (ab_lt.txt).
 #ifndef RT_LEAF_TESTS
-#define RT_LEAF_TESTS 1   // triangle tests per leaf trip of the BSP walk (1 or 2)
+#define RT_LEAF_TESTS 2   // triangle tests per leaf trip of the BSP walk: 1 or 2
 #endif
+template <bool COUNT, bool CULL>
+__device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const f3 o, const f3 d,
+                                               bool anyhit, Trav& t, Counters& c)
+{
+    if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
+        const v4u r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 16u, 0, 0);
+        const v4u r2 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
+        if (COUNT) {
+            c.v[C_IDS]++;
+            c.v[C_TESTS]++;
+        }
+        float dist, beta, gamma;
+        if (tri_math<true, COUNT, CULL>(as_f4(nx), as_f4(r1), as_f4(r2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+            if (COUNT) c.v[C_ACCEPTS]++;
+            t.tmax = dist;
+            t.found = true;
+            t.hit_k = t.leaf_k;
+            t.beta = beta;
+            t.gamma = gamma;
+        }
+        t.leaf_k += 48u;
+    }
+}
+
 template <bool COUNT, bool CULL = false>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
@@ -395,28 +430,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             t.gamma = gamma;
         }
         t.leaf_k += 48u;
-#if RT_LEAF_TESTS > 1
-        // a second test in the same trip: the next record's first 16 B are
-        // q3 (records are 48 B apart), its other 32 B one more round trip
-        if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
-            const v4u p1 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 16u, 0, 0);
-            const v4u p2 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
-            if (COUNT) {
-                c.v[C_IDS]++;
-                c.v[C_TESTS]++;
-            }
-            if (tri_math<true, COUNT, CULL>(as_f4(q3), as_f4(p1), as_f4(p2), o, d, t.tmin, t.tmax, dist, beta, gamma,
-                                             &c)) {
-                if (COUNT) c.v[C_ACCEPTS]++;
-                t.tmax = dist;
-                t.found = true;
-                t.hit_k = t.leaf_k;
-                t.beta = beta;
-                t.gamma = gamma;
-            }
-            t.leaf_k += 48u;
-        }
-#endif
+        if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c);
         const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
         done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
         pop = leaf_done & !t.found;
