@@ -392,6 +392,69 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
     }
 }
 
+// The leaf half of a BSP trip: test the record in q0..q2 (and, with
+// RT_LEAF_TESTS 2, the next one, whose first 16 B are q3).
+template <bool COUNT, bool CULL>
+__device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, const v4u q0, const v4u q1, const v4u q2,
+                                               const v4u q3, const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c,
+                                               bool& done, bool& pop)
+{
+    if (COUNT) {
+        c.v[C_IDS]++;
+        c.v[C_TESTS]++;
+    }
+    float dist, beta, gamma;
+    if (tri_math<true, COUNT, CULL>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+        if (COUNT) c.v[C_ACCEPTS]++;
+        t.tmax = dist;
+        t.found = true;
+        t.hit_k = t.leaf_k;
+        t.beta = beta;
+        t.gamma = gamma;
+    }
+    t.leaf_k += 48u;
+    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c);
+    const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
+    done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
+    pop = leaf_done & !t.found;
+}
+
+// The walking half of a BSP trip: node m (level 0), a child (level 1), a
+// grandchild (level 2) from the treelet in q0..q3.  Returns true when the walk
+// reached a non-empty leaf (its range is set, its tests start next trip); an
+// empty leaf sets pop.  (Testing the first record of a leaf in the trip that
+// reaches it -- one more round trip -- was slower: config 4 -3.7 %, config 5
+// -11 %, profiles/r02/ab_et1.txt.)
+template <bool COUNT>
+__device__ __forceinline__ bool bsp_walk(float* stk, const v4u q0, const v4u q1, const v4u q2, const v4u q3, const f3 o,
+                                         const f3 d, const f3 inv, Trav& t, Counters& c, bool& pop)
+{
+    uint32_t m = t.node;
+    const uint32_t dep = heap_depth(m);
+    uint2 n = make_uint2(q0.x, q0.y);
+    bool leaf = (n.x & 3u) == 3u;
+    if (!leaf) {
+        m = bsp_decide<COUNT>(stk, n, m, dep, o, d, inv, t, c);
+        n = (m & 1u) ? make_uint2(q1.x, q1.y) : make_uint2(q0.z, q0.w);
+        leaf = (n.x & 3u) == 3u;
+        if (!leaf) {
+            m = bsp_decide<COUNT>(stk, n, m, dep + 1u, o, d, inv, t, c);
+            const v4u g = (m & 2u) ? q3 : q2;
+            n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
+            leaf = (n.x & 3u) == 3u;
+            if (!leaf) m = bsp_decide<COUNT>(stk, n, m, dep + 2u, o, d, inv, t, c);
+        }
+    }
+    t.node = m;
+    if (leaf) {
+        if (COUNT) c.v[C_LEAF]++;
+        t.leaf_k = n.y;
+        t.leaf_end = n.y + (n.x >> 2);   // 48 * count
+        pop = (n.x >> 2) == 0u;
+    }
+    return leaf & !pop;
+}
+
 template <bool COUNT, bool CULL = false>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
@@ -399,8 +462,7 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
     const bool in_leaf = t.leaf_k != t.leaf_end;
-    uint32_t m = t.node;
-    const uint32_t base = in_leaf ? t.leaf_k : m << 6;
+    const uint32_t base = in_leaf ? t.leaf_k : t.node << 6;
     uint64_t tw = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
     v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
@@ -415,50 +477,8 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
     }
     bool done = false, pop = false;
-    if (in_leaf) {
-        if (COUNT) {
-            c.v[C_IDS]++;
-            c.v[C_TESTS]++;
-        }
-        float dist, beta, gamma;
-        if (tri_math<true, COUNT, CULL>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
-            if (COUNT) c.v[C_ACCEPTS]++;
-            t.tmax = dist;
-            t.found = true;
-            t.hit_k = t.leaf_k;
-            t.beta = beta;
-            t.gamma = gamma;
-        }
-        t.leaf_k += 48u;
-        if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c);
-        const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
-        done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
-        pop = leaf_done & !t.found;
-    } else {
-        // walk: node m (level 0), a child (level 1), a grandchild (level 2)
-        const uint32_t dep = heap_depth(m);
-        uint2 n = make_uint2(q0.x, q0.y);
-        bool leaf = (n.x & 3u) == 3u;
-        if (!leaf) {
-            m = bsp_decide<COUNT>(stk, n, m, dep, o, d, inv, t, c);
-            n = (m & 1u) ? make_uint2(q1.x, q1.y) : make_uint2(q0.z, q0.w);
-            leaf = (n.x & 3u) == 3u;
-            if (!leaf) {
-                m = bsp_decide<COUNT>(stk, n, m, dep + 1u, o, d, inv, t, c);
-                const v4u g = (m & 2u) ? q3 : q2;
-                n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
-                leaf = (n.x & 3u) == 3u;
-                if (!leaf) m = bsp_decide<COUNT>(stk, n, m, dep + 2u, o, d, inv, t, c);
-            }
-        }
-        t.node = m;
-        if (leaf) {
-            if (COUNT) c.v[C_LEAF]++;
-            t.leaf_k = n.y;
-            t.leaf_end = n.y + (n.x >> 2);   // 48 * count
-            pop = (n.x >> 2) == 0u;
-        }
-    }
+    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, o, d, anyhit, t, c, done, pop);
+    else bsp_walk<COUNT>(stk, q0, q1, q2, q3, o, d, inv, t, c, pop);
     if (pop) done = bsp_pop(stk, t);
     return done;
 }
