@@ -706,6 +706,9 @@ int rt_set_uniforms(rt_ctx* c, const rt_uniform* u, const float* jitter)
 {
     if (!c || !u) return RT_E_INVALID;
     if (u->resolution[0] == 0 || u->resolution[1] == 0) return fail(c, RT_E_INVALID, "rt_set_uniforms: zero resolution");
+    // k_path packs a lane's pixel as x | y << 16
+    if (u->resolution[0] > 65535u || u->resolution[1] > 65535u)
+        return fail(c, RT_E_INVALID, "rt_set_uniforms: resolution above 65535");
     if (u->subdivision_level == 0 || u->subdivision_level > 10)
         return fail(c, RT_E_INVALID, "rt_set_uniforms: subdivision_level must be in [1,10] (uniform.rs:36)");
     if (!jitter && u->subdivision_level != 1)

@@ -131,6 +131,48 @@ __device__ __forceinline__ Cam make_cam(const DevLaunch& L)
     c.aspect = L.cam[13];
     return c;
 }
+// Kernel arguments made opaque where a sample starts or a lane is refilled:
+// the values derived from them (the camera products, float resolutions,
+// integer-division reciprocals) are then recomputed there from SGPRs instead
+// of being hoisted out of the persistent loop into VGPRs that live across the
+// trip loop and are spilled (k_path at 8 waves/SIMD has 64 VGPRs).
+__device__ __forceinline__ uint32_t sopaque(uint32_t x)
+{
+    asm volatile("" : "+s"(x));
+    return x;
+}
+__device__ __forceinline__ float sopaque(float x)
+{
+    asm volatile("" : "+s"(x));
+    return x;
+}
+__device__ __forceinline__ Cam make_cam_opaque(const DevLaunch& L)
+{
+    Cam c = make_cam(L);
+    c.v = V(sopaque(c.v.x), sopaque(c.v.y), sopaque(c.v.z));
+    c.b1 = V(sopaque(c.b1.x), sopaque(c.b1.y), sopaque(c.b1.z));
+    c.b2 = V(sopaque(c.b2.x), sopaque(c.b2.y), sopaque(c.b2.z));
+    c.d = sopaque(c.d);
+    c.aspect = sopaque(c.aspect);
+    return c;
+}
+// The kernel argument blocks of k_path(DevScene, DevLaunch), re-read from
+// the kernarg segment through an opaque pointer where k_path shades and
+// refills: the fields used there are then scalar loads in that phase instead
+// of SGPRs (and VGPR lanes holding SGPR spills) kept across the trip loop.
+// (Taking the address of the parameters themselves would copy them to
+// scratch.)  The explicit arguments are laid out in order at their natural
+// alignment.
+constexpr size_t KARG_S = 0;
+constexpr size_t KARG_L = (sizeof(DevScene) + alignof(DevLaunch) - 1) & ~(alignof(DevLaunch) - 1);
+template <class T>
+__device__ __forceinline__ const T& kreload(size_t off)
+{
+    typedef __attribute__((address_space(4))) const char KC;
+    KC* p = (KC*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const T*)(p + off);   // generic; the address-space inference restores the scalar loads
+}
 __device__ __forceinline__ f3 cam_dir(const Cam& c, float ux, float uy, float jx, float jy)
 {
     return normalize(add(add(muls(muls(c.b1, ux + jx), c.aspect), muls(c.b2, uy + jy)), muls(c.v, c.d)));
@@ -145,8 +187,9 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
 {
     Pix p;
     const uint32_t lx = lane & 7u, ly = lane >> 3;
+    const uint32_t tiles_x = sopaque(L.tiles_x);   // see make_cam_opaque
     if (L.tileset == 0) {
-        uint32_t tx = work % L.tiles_x, ty = work / L.tiles_x;
+        uint32_t tx = work % tiles_x, ty = work / tiles_x;
         uint32_t rx = tx * 8u + lx, ry = ty * 8u + ly;
         p.valid = rx < L.w && ry < L.h;
         p.x = L.x0 + rx;
@@ -154,7 +197,7 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
         p.out = ry * L.w + rx;
     } else {
         uint32_t t = work * L.nranks + L.rank;
-        uint32_t tx = t % L.tiles_x, ty = t / L.tiles_x;
+        uint32_t tx = t % tiles_x, ty = t / tiles_x;
         p.x = tx * 8u + lx;
         p.y = ty * 8u + ly;
         p.valid = (t < L.tiles_x * L.tiles_y) && p.x < L.u.resolution[0] && p.y < L.u.resolution[1];
@@ -247,7 +290,7 @@ struct Trav {
     uint32_t node;   // BSP: 1-based heap index of the current node   BVH: stack top
     uint32_t lvl;    // BSP: bit trail (bit d = pending far child pushed at depth d)   BVH: pops so far
     uint32_t leaf_k, leaf_end;   // triangle slots of the leaf being tested (empty when equal)
-    float tmin, tmax, tmax0;
+    float tmin, tmax;
     bool found;
     uint32_t hit_k;
     float beta, gamma;
@@ -262,7 +305,6 @@ __device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
     t.leaf_k = t.leaf_end = 0;
     t.tmin = tmin;
     t.tmax = tmax;
-    t.tmax0 = tmax;
     t.found = false;
 }
 __device__ __forceinline__ TraceOut trav_out(const Trav& t) { return TraceOut{t.hit_k, t.beta, t.gamma, t.tmax}; }
@@ -279,11 +321,13 @@ __device__ __forceinline__ TraceOut trav_out(const Trav& t) { return TraceOut{t.
 // node at which the walk pushed its far child, so an entry is fully described
 // by its depth d: bit d of `lvl` marks it, the far child is the sibling of
 // the current node's ancestor at depth d+1, ((M >> (depth(M)-d-1)) ^ 1), and
-// only its t is stored -- in LDS, indexed by depth ([depth][thread], 4 B).
-// The tmax a pop restores is the t of the next pending entry below (or the
-// ray's original tmax): exactly the value bsp.wgsl saves in branch_ray.y,
-// since tmax only changes on push, pop, and on an accept, after which the
-// walk ends.
+// one float is stored -- in LDS, indexed by depth ([depth][thread], 4 B): the
+// tmax at the push, which is what bsp.wgsl saves in branch_ray.y and its pop
+// restores.  The other saved value, branch_ray.x = t, needs no slot: the push
+// sets tmax = t, tmax only changes on push, pop, and on an accept (after
+// which the walk ends), and every entry pushed above this one restores the
+// tmax it saw, so when this entry is popped the current tmax is its t, bit
+// for bit.  A pop is one LDS read.
 // anyhit: stop at the first accepted triangle -- shadow rays use only the
 // boolean, and the walk up to that triangle is identical, so it is too.
 // Interior nodes: the exact t = RN((plane - o)/denom) is only derived when the
@@ -297,8 +341,8 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
     const uint32_t d = heap_depth(t.lvl);
     t.lvl ^= 1u << d;
     t.node = (t.node >> (heap_depth(t.node) - d - 1u)) ^ 1u;
-    t.tmin = stk[d * 256u];
-    t.tmax = t.lvl ? stk[heap_depth(t.lvl) * 256u] : t.tmax0;
+    t.tmin = t.tmax;       // = the entry's t (see above)
+    t.tmax = stk[d * 256u];
     return false;
 }
 
@@ -306,9 +350,9 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 // One interior-node decision of bsp.wgsl:54-78 at node m (data n, depth dep).
 // Returns the next node.  Branch-free except for the exact division, which
 // only lanes whose approximate t cannot decide near/far take.  The push
-// stores t into the depth-dep slot unconditionally: no pending entry lives at
-// a depth >= depth(m) (they are all ancestors of m), so the store is dead
-// unless the trail bit is set.
+// stores the current tmax into the depth-dep slot unconditionally: no pending
+// entry lives at a depth >= depth(m) (they are all ancestors of m), so the
+// store is dead unless the trail bit is set.
 template <bool COUNT>
 __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, uint32_t dep, const f3 o,
                                                const f3 d, const f3 inv, Trav& t, Counters& c)
@@ -337,7 +381,7 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     const bool inside = amb & !(tt > t.tmax);
     const bool gofar = cfar | (inside & (tt < t.tmin));
     const bool push = inside & !(tt < t.tmin);
-    stk[dep * 256u] = tt;
+    stk[dep * 256u] = t.tmax;   // the tmax its pop restores
     t.lvl |= push ? 1u << dep : 0u;
     t.tmax = push ? tt : t.tmax;
     return gofar ? near_node ^ 1u : near_node;
@@ -973,8 +1017,9 @@ __device__ __forceinline__ f3 env_at(const DevLaunch& L, const f3 env, const f3 
     f3 e = env;
     if (RT_ENV_TEX && L.env_tex) {
         float rgb[3];
-        if (MODE == RT_MODE_W9E2) rt_det_env_sample_rgbe(L.env_tex, L.env_w, L.env_h, d.x, d.y, d.z, rgb);
-        else rt_det_env_sample(L.env_tex, L.env_w, L.env_h, d.x, d.y, d.z, rgb);
+        const uint32_t w = sopaque(L.env_w), h = sopaque(L.env_h);   // see make_cam_opaque
+        if (MODE == RT_MODE_W9E2) rt_det_env_sample_rgbe(L.env_tex, w, h, d.x, d.y, d.z, rgb);
+        else rt_det_env_sample(L.env_tex, w, h, d.x, d.y, d.z, rgb);
         e = V(rgb[0], rgb[1], rgb[2]);
     }
     return e;
@@ -1094,16 +1139,7 @@ k_path(DevScene S, DevLaunch L)
     constexpr uint32_t MAXD = W8E1 ? 10u : 50u;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
-    const Cam cam = make_cam(L);
-    const float fH = (float)L.u.resolution[1];
-    const uint32_t resx = L.u.resolution[0];
-    const uint32_t light_tris = S.nlights - 1u;
-    const uint32_t sel = W9 ? L.u.selection1 : 0u;
-    const uint32_t it_end = L.first_iter + L.spp;
-    const uint32_t pslots = L.nwork * 64u;            // pixel slots
-    const uint32_t nslots = pslots * L.nchunks;       // work units (host keeps this < 2^31)
     const uint32_t T = L.shade_threshold;
-    const f3 env = V(L.env[0], L.env[1], L.env[2]);
     Counters cnt;
 #pragma unroll
     for (int i = 0; i < C_N; i++) cnt.v[i] = 0;
@@ -1113,7 +1149,8 @@ k_path(DevScene S, DevLaunch L)
     uint32_t st = ST_IDLE;
     bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false, ao = false, hblk = false;
     uint32_t hph = 0;   // W9E3 holdout: 1 = occlusion ray in flight, 2 = sun ray in flight
-    uint32_t px = 0, py = 0, out = 0, it = 0, unit_end = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
+    // pxy: the pixel as x | y << 16 (the host keeps the resolution below 2^16)
+    uint32_t pxy = 0, out = 0, it = 0, unit_end = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
     f3 res = V(0, 0, 0), fac = V(1, 1, 1), ro = V(0, 0, 0), rd = V(0, 0, 1), inv = V(0, 0, 0);
     f3 ndir = V(0, 0, 1), cu = V(0, 0, 0), cb = V(0, 0, 0);
     Trav tr;
@@ -1121,14 +1158,20 @@ k_path(DevScene S, DevLaunch L)
 
 
     // fs_main prologue for iteration `it` of the lane's pixel (w7e3.wgsl:236-248)
-    auto start_sample = [&]() {
-        rng = tea16(py * resx + px, it);
+    auto start_sample = [&](const DevLaunch& L) {
+        const uint32_t px = pxy & 0xFFFFu, py = pxy >> 16;
+        rt_uniform u;
+        u.resolution[0] = sopaque(L.u.resolution[0]);
+        u.resolution[1] = sopaque(L.u.resolution[1]);
+        const float fH = (float)u.resolution[1];
+        const Cam cam = make_cam_opaque(L);
+        rng = tea16(py * u.resolution[0] + px, it);
         float jx = rnd(rng);
         float jy = rnd(rng);
         jx = jx / fH;
         jy = jy / fH;
         float ux, uy;
-        pixel_uv(L.u, px, py, ux, uy);
+        pixel_uv(u, px, py, ux, uy);
         rd = cam_dir(cam, ux, uy, jx, jy);
         ro = cam.e;
         res = V(0, 0, 0);
@@ -1191,6 +1234,18 @@ k_path(DevScene S, DevLaunch L)
             if (st == ST_SHADE) cnt.v[C_SHADE_LANES]++;
             tstamp = now;
         }
+        {
+        // the shading and refill phases read the kernel arguments afresh (kreload)
+        const DevScene& Sk = kreload<DevScene>(KARG_S);
+        const DevLaunch& Lk = kreload<DevLaunch>(KARG_L);
+        const DevScene& S = Sk;
+        const DevLaunch& L = Lk;
+        const uint32_t light_tris = S.nlights - 1u;
+        const uint32_t sel = W9 ? L.u.selection1 : 0u;
+        const uint32_t it_end = L.first_iter + L.spp;
+        const uint32_t pslots = L.nwork * 64u;            // pixel slots
+        const uint32_t nslots = pslots * L.nchunks;       // work units (host keeps this < 2^31)
+        const f3 env = V(L.env[0], L.env[1], L.env[2]);
         // ---- shading phase
         if (st == ST_SHADE) {
             bool sample_done = false;
@@ -1224,6 +1279,11 @@ k_path(DevScene S, DevLaunch L)
                             cu = V(rt_minf(cu.x, 100.0f), rt_minf(cu.y, 100.0f), rt_minf(cu.z, 100.0f));
                             cb = V(rt_minf(cb.x, 100.0f), rt_minf(cb.y, 100.0f), rt_minf(cb.z, 100.0f));
                         }
+                        // both outcomes' sums now (the same additions the shadow
+                        // result would select): res carries the unblocked one and cb
+                        // the blocked one across the shadow walk, 3 floats fewer
+                        cb = add(res, cb);
+                        res = add(res, cu);
                         fac = mul(fac, muls(brdf, RT_PI_F));
                         const float prob = (brdf.x + brdf.y + brdf.z) / 3.0f;
                         survive = !W8E1 && rnd(rng) < prob;   // w8e1.wgsl: direct light only
@@ -1393,7 +1453,7 @@ k_path(DevScene S, DevLaunch L)
                 sample_done = true;
             } else {
                 // shadow ray finished: rest of lambertian, then the bounce
-                res = add(res, tr.found ? cb : cu);
+                if (tr.found) res = cb;
                 if (survive && bounce + 1u < MAXD) {
                     rd = ndir;   // origin = hit position, already in ro
                     inv = trav_inv<TRAV>(rd);
@@ -1415,7 +1475,7 @@ k_path(DevScene S, DevLaunch L)
                 const v4f sv = {res.x, res.y, res.z, __uint_as_float(prim)};
                 __builtin_nontemporal_store(sv, sp);
                 it++;
-                if (it < unit_end) start_sample();
+                if (it < unit_end) start_sample(L);
                 else st = ST_IDLE;
             }
         }
@@ -1460,21 +1520,21 @@ k_path(DevScene S, DevLaunch L)
                     // pixels at the same iteration; pixel-major (1): the iterations
                     // of one pixel side by side
                     uint32_t ch, ps;
+                    const uint32_t psl = sopaque(L.nwork) * 64u, nch = sopaque(L.nchunks);
                     if (L.unit_order == 0u) {
-                        ch = slot / pslots;
-                        ps = slot - ch * pslots;
+                        ch = slot / psl;
+                        ps = slot - ch * psl;
                     } else {
-                        ps = slot / L.nchunks;
-                        ch = slot - ps * L.nchunks;
+                        ps = slot / nch;
+                        ch = slot - ps * nch;
                     }
                     const Pix p = map_pixel(L, ps >> 6, ps & 63u);
                     if (p.valid) {
-                        px = p.x;
-                        py = p.y;
+                        pxy = p.x | p.y << 16;
                         out = p.out;
                         it = L.first_iter + ch * L.chunk;
                         unit_end = it + L.chunk < it_end ? it + L.chunk : it_end;
-                        start_sample();
+                        start_sample(L);
                     }
                 }
             }
@@ -1482,6 +1542,7 @@ k_path(DevScene S, DevLaunch L)
                 shard = (shard + 1u) & ((1u << LGSH) - 1u);
                 if (++tried == (1u << LGSH)) exhausted = true;
             }
+        }
         }
         if (COUNT) {
             const uint64_t now = __builtin_amdgcn_s_memtime();

@@ -282,3 +282,13 @@ def test_display_frame_rgba8(rt):
     assert np.all((img[..., :3] == ref) | near)
     assert np.all(img[..., 3] == 255)
     rs.ctx.close()
+
+
+def test_resolution_limit(rt, gpu):
+    # k_path packs a lane's pixel as x | y << 16: larger frames are refused
+    # at the boundary, not rendered wrongly
+    with pytest.raises(rt.RtError):
+        gpu.set_uniforms(rt.make_uniform(*BASIC_CAM, 65536, 16))
+    with pytest.raises(rt.RtError):
+        gpu.set_uniforms(rt.make_uniform(*BASIC_CAM, 16, 65536))
+    gpu.set_uniforms(rt.make_uniform(*BASIC_CAM, 65535, 16))
