@@ -205,6 +205,15 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
     }
     return p;
 }
+// map_pixel's output index recomputed from the pixel (k_path keeps only the
+// pixel across the trip loop): region mode ry * w + rx; tileset mode the
+// packed slot work * 64 + lane of tile t = work * nranks + rank.
+__device__ __forceinline__ uint32_t pixel_out(const DevLaunch& L, uint32_t x, uint32_t y)
+{
+    if (L.tileset == 0) return (y - L.y0) * L.w + (x - L.x0);
+    const uint32_t t = (y >> 3) * L.tiles_x + (x >> 3);
+    return (t - L.rank) / L.nranks * 64u + ((y & 7u) << 3) + (x & 7u);
+}
 // The XCD this wave runs on (HW_REG_XCC_ID, hwreg 20, bits 3:0; 0-7 on MI355X):
 // the k_path work shard.  Any value is correct, only the atomic spread changes.
 __device__ __forceinline__ uint32_t shard_of_wave()
@@ -1150,7 +1159,7 @@ k_path(DevScene S, DevLaunch L)
     bool exhausted = L.spp == 0u, shadow = false, emit = true, survive = false, ao = false, hblk = false;
     uint32_t hph = 0;   // W9E3 holdout: 1 = occlusion ray in flight, 2 = sun ray in flight
     // pxy: the pixel as x | y << 16 (the host keeps the resolution below 2^16)
-    uint32_t pxy = 0, out = 0, it = 0, unit_end = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
+    uint32_t pxy = 0, it = 0, prim = 0xFFFFFFFFu, rng = 0, bounce = 0;
     f3 res = V(0, 0, 0), fac = V(1, 1, 1), ro = V(0, 0, 0), rd = V(0, 0, 1), inv = V(0, 0, 0);
     f3 ndir = V(0, 0, 1), cu = V(0, 0, 0), cb = V(0, 0, 0);
     Trav tr;
@@ -1471,11 +1480,14 @@ k_path(DevScene S, DevLaunch L)
                 // this iteration's `result` (+ primary id); k_fold accumulates in
                 // iteration order (w7e3.wgsl:261-271).  Streaming store: keep the
                 // scene, not the samples, in L2/MALL.
+                const uint32_t out = pixel_out(L, pxy & 0xFFFFu, pxy >> 16);
                 v4f* sp = reinterpret_cast<v4f*>(L.samples + (size_t)(it - L.first_iter) * L.stride + out);
                 const v4f sv = {res.x, res.y, res.z, __uint_as_float(prim)};
                 __builtin_nontemporal_store(sv, sp);
                 it++;
-                if (it < unit_end) start_sample(L);
+                // the unit's end, from its chunk (it - 1 lies in it)
+                const uint32_t ue = L.first_iter + ((it - 1u - L.first_iter) / L.chunk + 1u) * L.chunk;
+                if (it < (ue < it_end ? ue : it_end)) start_sample(L);
                 else st = ST_IDLE;
             }
         }
@@ -1531,9 +1543,7 @@ k_path(DevScene S, DevLaunch L)
                     const Pix p = map_pixel(L, ps >> 6, ps & 63u);
                     if (p.valid) {
                         pxy = p.x | p.y << 16;
-                        out = p.out;
                         it = L.first_iter + ch * L.chunk;
-                        unit_end = it + L.chunk < it_end ? it + L.chunk : it_end;
                         start_sample(L);
                     }
                 }
