@@ -1481,7 +1481,12 @@ k_path(DevScene S, DevLaunch L)
                 // iteration order (w7e3.wgsl:261-271).  Streaming store: keep the
                 // scene, not the samples, in L2/MALL.
                 const uint32_t out = pixel_out(L, pxy & 0xFFFFu, pxy >> 16);
-                v4f* sp = reinterpret_cast<v4f*>(L.samples + (size_t)(it - L.first_iter) * L.stride + out);
+                // record layout follows the unit order: pixel-major units keep a
+                // pixel's iterations together ([pixel][iteration]), so the lanes of a
+                // refill (one pixel, consecutive iterations) write whole lines
+                const uint32_t ip = it - L.first_iter;
+                const size_t ri = L.unit_order ? (size_t)out * L.spp + ip : (size_t)ip * L.stride + out;
+                v4f* sp = reinterpret_cast<v4f*>(L.samples + ri);
                 const v4f sv = {res.x, res.y, res.z, __uint_as_float(prim)};
                 __builtin_nontemporal_store(sv, sp);
                 it++;
@@ -1569,8 +1574,11 @@ k_path(DevScene S, DevLaunch L)
 // for iterations first_iter .. first_iter+spp-1 in order to each output pixel:
 // accum = max(vec4((result + prev*it)/(it+1), 1), 0) with prev the stored
 // accumulation (read when first_iter > 0, as the RenderSource texture).  One
-// thread per pixel; samples are [iteration][pixel] so a wave reads 1 KiB
-// contiguous per iteration.  ids = primary hit of the last iteration.
+// thread per pixel.  Chunk-major units write samples as [iteration][pixel] (a
+// wave reads 1 KiB contiguous per iteration); pixel-major units (the default)
+// as [pixel][iteration], so k_path's 16-B records land in whole lines and a
+// thread here streams its own pixel's records.  ids = primary hit of the last
+// iteration.
 __global__ void __launch_bounds__(256) k_fold(DevLaunch L)
 {
     const uint32_t nout = L.tileset ? L.nwork * 64u : L.w * L.h;
@@ -1584,14 +1592,38 @@ __global__ void __launch_bounds__(256) k_fold(DevLaunch L)
             a2 = pa.z;
         }
         v4f r = {0.0f, 0.0f, 0.0f, 0.0f};
-        const v4f* sp = reinterpret_cast<const v4f*>(L.samples + o);
-        for (uint32_t i = 0; i < L.spp; i++) {
-            r = __builtin_nontemporal_load(sp + (size_t)i * L.stride);
+        auto fold1 = [&](const v4f x, uint32_t i) {
             const uint32_t it = L.first_iter + i;
             const float fi = (float)it, fi1 = (float)(it + 1u);
-            a0 = rt_max0f((r.x + a0 * fi) / fi1);
-            a1 = rt_max0f((r.y + a1 * fi) / fi1);
-            a2 = rt_max0f((r.z + a2 * fi) / fi1);
+            a0 = rt_max0f((x.x + a0 * fi) / fi1);
+            a1 = rt_max0f((x.y + a1 * fi) / fi1);
+            a2 = rt_max0f((x.z + a2 * fi) / fi1);
+        };
+        uint32_t i = 0;
+        if (L.unit_order) {
+            // [pixel][iteration]: the thread's own records are contiguous; eight
+            // (128 B) are loaded together, so each line is fetched once while the
+            // wave's 64 threads stream 64 lines side by side
+            const v4f* sp = reinterpret_cast<const v4f*>(L.samples + (size_t)o * L.spp);
+            for (; i + 8u <= L.spp; i += 8u) {
+                v4f q[8];
+#pragma unroll
+                for (int k = 0; k < 8; k++) q[k] = sp[i + k];
+#pragma unroll
+                for (int k = 0; k < 8; k++) fold1(q[k], i + k);
+                r = q[7];
+            }
+            for (; i < L.spp; i++) {
+                r = sp[i];
+                fold1(r, i);
+            }
+        } else {
+            // [iteration][pixel]: a wave reads 1 KiB contiguous per iteration
+            const v4f* sp = reinterpret_cast<const v4f*>(L.samples + o);
+            for (; i < L.spp; i++) {
+                r = __builtin_nontemporal_load(sp + (size_t)i * L.stride);
+                fold1(r, i);
+            }
         }
         L.accum[o] = make_float4(a0, a1, a2, 1.0f);
         if (L.ids && L.spp) L.ids[o] = __float_as_uint(r.w);
