@@ -61,3 +61,14 @@ def test_two_rank_bench_frame_equals_one_rank(tmp_path, rt, oracle):
     o = oracle.render(sc, oracle.make_uniform(*wl.camera, W, H), wl.mode, "BSP", (0, 0, W, H), 0, SPP)
     linf, bits, idm = compare((f2["accum"], f2["ids"], None), o)
     assert idm == 0 and bits == 0, (idm, bits, linf)
+
+
+def test_eight_rank_bench_frame_equals_one_rank(tmp_path):
+    # the driver's largest launch (8 ranks), rehearsed on the one GPU: 425 tiles
+    # dealt to 8 ranks (53 or 54 each), gathered to rank 0 and unpacked
+    one, f1 = _bench(1, str(tmp_path / "n1.npz"))
+    eight, f8 = _bench(8, str(tmp_path / "n8.npz"))
+    assert eight["n_gpus"] == 8 and eight["config"]["world_size"] == 8
+    assert eight["rays_per_step"] == one["rays_per_step"]
+    assert np.array_equal(f1["ids"], f8["ids"])
+    assert np.array_equal(f1["accum"].view(np.uint32), f8["accum"].view(np.uint32))
