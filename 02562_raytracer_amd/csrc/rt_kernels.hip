@@ -437,9 +437,11 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
-            t.hit_k = t.leaf_k;
-            t.beta = beta;
-            t.gamma = gamma;
+            // an any-hit walk keeps the hit it started from (k_path redraws from
+            // it); selects, not a branch (no exec-mask work in the trip)
+            t.hit_k = anyhit ? t.hit_k : t.leaf_k;
+            t.beta = anyhit ? t.beta : beta;
+            t.gamma = anyhit ? t.gamma : gamma;
         }
         t.leaf_k += 48u;
     }
@@ -461,9 +463,9 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
         if (COUNT) c.v[C_ACCEPTS]++;
         t.tmax = dist;
         t.found = true;
-        t.hit_k = t.leaf_k;
-        t.beta = beta;
-        t.gamma = gamma;
+        t.hit_k = anyhit ? t.hit_k : t.leaf_k;
+        t.beta = anyhit ? t.beta : beta;
+        t.gamma = anyhit ? t.gamma : gamma;
     }
     t.leaf_k += 48u;
     if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c);
@@ -686,9 +688,11 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
-            t.hit_k = t.leaf_k;
-            t.beta = beta;
-            t.gamma = gamma;
+            // an any-hit walk keeps the hit it started from (k_path redraws from
+            // it); selects, not a branch (no exec-mask work in the trip)
+            t.hit_k = anyhit ? t.hit_k : t.leaf_k;
+            t.beta = anyhit ? t.beta : beta;
+            t.gamma = anyhit ? t.gamma : gamma;
         }
         t.leaf_k += 48u;
         if (anyhit & t.found) return true;
@@ -787,6 +791,8 @@ __device__ __forceinline__ bool trace(const DevScene& S, void* stk, const BvhDee
                                       float tmin, float tmax, bool anyhit, TraceOut& out, Counters& c)
 {
     Trav t;
+    t.hit_k = 0;   // an any-hit walk leaves the hit record alone
+    t.beta = t.gamma = 0.0f;
     trav_start<TRAV>(t, stk, tmin, tmax);
     const f3 inv = trav_inv<TRAV>(d);
     for (uint32_t guard = 0; guard < (1u << 24); guard++)
@@ -1146,6 +1152,11 @@ k_path(DevScene S, DevLaunch L)
     constexpr bool CLAMP = W8 && !W8E1;
     constexpr bool FAC_AMB = W9 || W8E3;   // ambient = emission * factor
     constexpr uint32_t MAXD = W8E1 ? 10u : 50u;
+    // W9E1 draws the next bounce direction after the shadow walk, from the hit
+    // the any-hit walk left in the traversal state (resolve() again): the shadow
+    // walk draws no random numbers, so the PRNG sequence is the reference's, and
+    // the direction (3 floats) need not be kept across the walk
+    constexpr bool REDRAW = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t T = L.shade_threshold;
@@ -1297,7 +1308,7 @@ k_path(DevScene S, DevLaunch L)
                         const float prob = (brdf.x + brdf.y + brdf.z) / 3.0f;
                         survive = !W8E1 && rnd(rng) < prob;   // w8e1.wgsl: direct light only
                         if (survive && bounce + 1u < MAXD) {
-                            ndir = indirect_dir(h.nrm, rng);   // setup_indirect (:472-489)
+                            if (!REDRAW) ndir = indirect_dir(h.nrm, rng);   // setup_indirect (:472-489)
                             fac = divs(fac, prob);
                         }
                         // shadow ray (ray_init + tmin/tmax override, :442-449)
@@ -1464,7 +1475,8 @@ k_path(DevScene S, DevLaunch L)
                 // shadow ray finished: rest of lambertian, then the bounce
                 if (tr.found) res = cb;
                 if (survive && bounce + 1u < MAXD) {
-                    rd = ndir;   // origin = hit position, already in ro
+                    if (REDRAW) rd = indirect_dir(resolve<TRAV>(S, trav_out(tr), ro, rd, !W9).nrm, rng);
+                    else rd = ndir;   // origin = hit position, already in ro
                     inv = trav_inv<TRAV>(rd);
                     trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
                     emit = false;

@@ -42,8 +42,8 @@ def device_asm(tmp_path_factory):
 WHOLE_BUDGET = {
     # (round 2: 148/133, 152/116 and 8/2 before the kernel arguments were
     # re-read in the shading phase and the shading state was trimmed)
-    "k_pathILi4ELi0ELb0": (88, 92),     # W9E1, BSP
-    "k_pathILi4ELi1ELb0": (88, 88),     # W9E1, BVH
+    "k_pathILi4ELi0ELb0": (68, 70),     # W9E1, BSP
+    "k_pathILi4ELi1ELb0": (76, 71),     # W9E1, BVH
     "k_pathILi3ELi0ELb0": (0, 0),       # W7E3, BSP at 5 waves/SIMD
 }
 
