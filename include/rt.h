@@ -243,7 +243,9 @@ int rt_upload_bvh(rt_ctx* ctx, const rt_gpu_node* nodes, uint32_t nnodes,
 
 /* Uniforms + jitter table (src/bindings/uniform.rs:163-176).  jitter holds
  * subdivision_level^2 float2 offsets (may be NULL when subdivision_level == 1:
- * compute_jitters returns (0,0), uniform.rs:261-263). */
+ * compute_jitters returns (0,0), uniform.rs:261-263).  RT_E_INVALID for a zero
+ * resolution or one above 65535 in either axis (the path kernel packs a pixel's
+ * coordinates into one 32-bit register). */
 int rt_set_uniforms(rt_ctx* ctx, const rt_uniform* u, const float* jitter);
 
 /* ---- acceleration-structure construction on the GPU ---- */
