@@ -1509,18 +1509,22 @@ k_path(DevScene S, DevLaunch L)
             }
         }
         // ---- refill idle lanes with new pixels (ballot + mbcnt compaction).
-        //      BVH walk: the slots are dealt round-robin to 8 shards, one per
-        //      XCD, each with its own queue head in its own 128-B line, so the
-        //      refills of 256 CUs do not all meet on one atomic (+22 % on the
-        //      config-3 BVH frame).  The shard is the XCD id read from the
-        //      hardware at each refill; a shard's slots are equal in number and
-        //      interleaved over the frame, so the shards drain together; a wave
-        //      whose home shard is drained moves on to the next ones (restarting
-        //      from home at each refill), so every slot is handed out whatever
-        //      XCDs the waves land on.  The BSP walk keeps one queue: it gained
-        //      nothing from shards, and any shard address here pushed its trip
-        //      loop into spills (tests/test_isa_guard.py).
-        constexpr uint32_t LGSH = TRAV == RT_TRAVERSE_BVH ? 3u : 0u;
+        //      The slots are dealt to 8 shards, one per XCD, each with its own
+        //      queue head in its own 128-B line, so the refills of 256 CUs do not
+        //      all meet on one atomic: a shard owns every 8th block of 64
+        //      consecutive slots (a refill's worth, so a refill still hands out
+        //      neighbouring units).  The shard is the XCD id read from the
+        //      hardware at each refill; the shards' blocks interleave over the
+        //      frame, so they drain together; a wave whose home shard is drained
+        //      moves on to the next ones (restarting from home at each refill), so
+        //      every slot is handed out whatever XCDs the waves land on.  One
+        //      global queue cost config 2 (short Cornell-box rays, many refills)
+        //      39 % of its frame; interleaving single slots instead of blocks cost
+        //      config 4 at 16 spp 13 % (profiles/r02/ab_shards.txt).
+#ifndef RT_BSP_SHARDS_LG
+#define RT_BSP_SHARDS_LG 3
+#endif
+        constexpr uint32_t LGSH = TRAV == RT_TRAVERSE_BVH ? 3u : RT_BSP_SHARDS_LG;
         uint32_t shard = LGSH ? shard_of_wave() : 0u;
         uint32_t tried = 0;
         for (;;) {
@@ -1531,16 +1535,19 @@ k_path(DevScene S, DevLaunch L)
             if (lane == leader) {
                 const uint32_t head = atomicAdd(L.work_counter + shard * 32u, (uint32_t)__popcll(need));
                 // a drained shard's head keeps growing with every futile draw:
-                // clamp before the shift so the slot cannot wrap
-                const uint32_t len = (nslots - shard + (1u << LGSH) - 1u) >> LGSH;
-                base = LGSH == 0u ? head : head < len ? (head << LGSH) + shard : nslots;
+                // clamp it so the slot below cannot wrap (nslots < 2^31)
+                base = LGSH == 0u ? head : head < (1u << 28) ? head : (1u << 28);
             }
             base = __shfl(base, (int)leader, 64);
             bool ran_out = false;
             if (st == ST_IDLE && !exhausted) {
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
-                const uint32_t slot = base + (rank << LGSH);
+                // position h of the shard's sequence; the shard owns every
+                // 2^LGSH-th block of 64 consecutive slots, so one refill still hands
+                // out neighbouring units (pixel-major: the iterations of one pixel)
+                const uint32_t h = base + rank;
+                const uint32_t slot = LGSH == 0u ? h : ((((h >> 6) << LGSH) + shard) << 6) | (h & 63u);
                 if (slot >= nslots) {
                     if (LGSH == 0u) exhausted = true;
                     else ran_out = true;
