@@ -834,7 +834,10 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     }
     // default shading threshold per walk (BSP sweep 8 best;
     // BVH 2-4 best, 4695 vs 4604 Mrays/s at 8)
-    L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold : trav == RT_TRAVERSE_BVH ? 4 : 8);
+    // defaults per walk and shader (profiles/r02/ab_w7e3_shards.txt: W7E3's short
+    // Cornell-box rays shade often, and refilling earlier pays there)
+    L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold
+                                   : trav == RT_TRAVERSE_BVH ? 4 : mode == RT_MODE_W7E3 ? 24 : 8);
     L.reserved0 = 0;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));

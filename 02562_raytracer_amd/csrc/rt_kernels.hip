@@ -933,9 +933,12 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 // W7E3 (config 2): its area-light shading keeps more state than W9E1's.  At 8
 // waves/SIMD (64 VGPRs) it spilled 272 B per lane and moved 103 GB per config-2
 // launch through L2 for 1 GB of sample records; at 5 (96 VGPRs) 76 B and 10 GB,
-// and the frame is 3.5 % faster: 4528 vs 4375 Mrays/s (profiles/r02/ab_w7e3_waves.txt)
+// and the frame is 3.5 % faster: 4528 vs 4375 Mrays/s (profiles/r02/ab_w7e3_waves.txt).
+// With the round-2 spill cuts and per-XCD work shards, 7 waves (72 VGPRs, 52 B of
+// scratch per lane) is the best: 8500 vs 7866 (5) and 8205 (8) Mrays/s
+// (profiles/r02/ab_w7e3_shards.txt)
 #ifndef RT_W7E3_WAVES_PER_EU
-#define RT_W7E3_WAVES_PER_EU 5
+#define RT_W7E3_WAVES_PER_EU 7
 #endif
 // traversal steps per shading-threshold check in k_path's trip loop
 // (profiles/r02/ab_tpc2.txt: 2 vs 1 = config 3 +1.4%, BVH +2.6%, config 2 +0.6%;

@@ -21,6 +21,7 @@ BUDGET = {
     # (RT_TRIPS_PER_CHECK); none of them spills
     "k_pathILi4ELi0ELb0": 0,
     "k_pathILi4ELi1ELb0": 0,   # W9E1, BVH at 8 waves/SIMD (4 before the round-2 spill cuts)
+    "k_pathILi3ELi0ELb0": 0,   # W7E3, BSP at 7 waves/SIMD
 }
 
 
@@ -44,7 +45,7 @@ WHOLE_BUDGET = {
     # re-read in the shading phase and the shading state was trimmed)
     "k_pathILi4ELi0ELb0": (68, 70),     # W9E1, BSP
     "k_pathILi4ELi1ELb0": (76, 71),     # W9E1, BVH
-    "k_pathILi3ELi0ELb0": (0, 0),       # W7E3, BSP at 5 waves/SIMD
+    "k_pathILi3ELi0ELb0": (52, 30),     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
 }
 
 
