@@ -1627,13 +1627,16 @@ __global__ void __launch_bounds__(256) k_fold(DevLaunch L)
             // (128 B) are loaded together, so each line is fetched once while the
             // wave's 64 threads stream 64 lines side by side
             const v4f* sp = reinterpret_cast<const v4f*>(L.samples + (size_t)o * L.spp);
-            for (; i + 8u <= L.spp; i += 8u) {
-                v4f q[8];
+#ifndef RT_FOLD_BATCH
+#define RT_FOLD_BATCH 8
+#endif
+            for (; i + RT_FOLD_BATCH <= L.spp; i += RT_FOLD_BATCH) {
+                v4f q[RT_FOLD_BATCH];
 #pragma unroll
-                for (int k = 0; k < 8; k++) q[k] = sp[i + k];
+                for (int k = 0; k < RT_FOLD_BATCH; k++) q[k] = sp[i + k];
 #pragma unroll
-                for (int k = 0; k < 8; k++) fold1(q[k], i + k);
-                r = q[7];
+                for (int k = 0; k < RT_FOLD_BATCH; k++) fold1(q[k], i + k);
+                r = q[RT_FOLD_BATCH - 1];
             }
             for (; i < L.spp; i++) {
                 r = sp[i];
