@@ -210,7 +210,7 @@ int rt_create(int device, rt_ctx** out)
     memset(&c->u, 0, sizeof c->u);
     memset(&c->last, 0, sizeof c->last);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess ||
-        c->work.alloc(1024) != hipSuccess || c->counters.alloc(32 * sizeof(unsigned long long)) != hipSuccess) {
+        c->work.alloc(4096) != hipSuccess || c->counters.alloc(32 * sizeof(unsigned long long)) != hipSuccess) {
         delete c;
         return fail(nullptr, RT_E_DEVICE, "rt_create: stream/buffer setup failed");
     }
@@ -865,13 +865,13 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
             L.chunk = ch;
             L.unit_order = c->unit_order;
             L.nchunks = (L.spp + ch - 1) / ch;
-            HIPCHK(c, hipMemsetAsync(c->work.p, 0, 1024, c->stream));
+            HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
             if (int r = launch_timed(c, S, L, mode, trav)) return r;
             const int r = rtk::launch_fold(L, c->stream);
             if (r) return fail(c, r, std::string("fold launch failed: ") + hipGetErrorString(hipGetLastError()));
         }
     } else {
-        HIPCHK(c, hipMemsetAsync(c->work.p, 0, 1024, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
         if (int r = launch_timed(c, S, L, mode, trav)) return r;
     }
     if (counts) return rt_last_counts(c, counts);

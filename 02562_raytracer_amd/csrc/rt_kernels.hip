@@ -214,11 +214,20 @@ __device__ __forceinline__ uint32_t pixel_out(const DevLaunch& L, uint32_t x, ui
     const uint32_t t = (y >> 3) * L.tiles_x + (x >> 3);
     return (t - L.rank) / L.nranks * 64u + ((y & 7u) << 3) + (x & 7u);
 }
-// The XCD this wave runs on (HW_REG_XCC_ID, hwreg 20, bits 3:0; 0-7 on MI355X):
-// the k_path work shard.  Any value is correct, only the atomic spread changes.
+// The work shard of this wave: the XCD it runs on (HW_REG_XCC_ID, hwreg 20,
+// bits 3:0; 0-7 on MI355X), and with RT_SHARD_LG > 3 also the low bits of its
+// CU id within the XCD (HW_REG_HW_ID, hwreg 4, bits 11:8).  Any value is
+// correct, only the atomic spread changes.
+#ifndef RT_SHARD_LG
+#define RT_SHARD_LG 3
+#endif
 __device__ __forceinline__ uint32_t shard_of_wave()
 {
-    return (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | ((3 - 1) << 11)) & 7u;
+    const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | ((3 - 1) << 11)) & 7u;
+    if (RT_SHARD_LG <= 3) return xcc;
+    const uint32_t cu = ((uint32_t)__builtin_amdgcn_s_getreg(4 | (8 << 6) | ((4 - 1) << 11))) & 15u;
+    constexpr uint32_t SUB = RT_SHARD_LG > 3 ? RT_SHARD_LG - 3 : 0;
+    return (xcc << SUB) | (cu & ((1u << SUB) - 1u));
 }
 
 __device__ __forceinline__ uint32_t fetch_work(uint32_t* ctr, uint32_t lane)
@@ -1525,9 +1534,9 @@ k_path(DevScene S, DevLaunch L)
         //      39 % of its frame; interleaving single slots instead of blocks cost
         //      config 4 at 16 spp 13 % (profiles/r02/ab_shards.txt).
 #ifndef RT_BSP_SHARDS_LG
-#define RT_BSP_SHARDS_LG 3
+#define RT_BSP_SHARDS_LG RT_SHARD_LG
 #endif
-        constexpr uint32_t LGSH = TRAV == RT_TRAVERSE_BVH ? 3u : RT_BSP_SHARDS_LG;
+        constexpr uint32_t LGSH = TRAV == RT_TRAVERSE_BVH ? RT_SHARD_LG : RT_BSP_SHARDS_LG;
         uint32_t shard = LGSH ? shard_of_wave() : 0u;
         uint32_t tried = 0;
         for (;;) {
