@@ -21,7 +21,7 @@ def main():
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--trav", default=None)
-    ap.add_argument("--chunks", default="4")
+    ap.add_argument("--chunks", default="1")   # the bench's one-iteration units
     args = ap.parse_args()
     import torch
     rt = importlib.import_module("02562_raytracer_amd")
