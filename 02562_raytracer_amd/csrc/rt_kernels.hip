@@ -20,6 +20,7 @@
 //     48-B records {v0, e0, e1, n} in treeIds order (one 3 x dwordx4 gather).
 // Numerics: -ffp-contract=off, correctly rounded f32 div/sqrt, pinned
 // transcendentals (include/rt_detmath.h) => bit-identical to the CPU oracle.
+#include <type_traits>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -163,6 +164,10 @@ __device__ __forceinline__ Cam make_cam_opaque(const DevLaunch& L)
 // (Taking the address of the parameters themselves would copy them to
 // scratch.)  The explicit arguments are laid out in order at their natural
 // alignment.
+// Every GPU parity test reads both blocks through these offsets (a wrong one
+// would change every frame).
+static_assert(std::is_standard_layout<DevScene>::value && std::is_trivially_copyable<DevScene>::value, "DevScene");
+static_assert(std::is_standard_layout<DevLaunch>::value && std::is_trivially_copyable<DevLaunch>::value, "DevLaunch");
 constexpr size_t KARG_S = 0;
 constexpr size_t KARG_L = (sizeof(DevScene) + alignof(DevLaunch) - 1) & ~(alignof(DevLaunch) - 1);
 template <class T>
