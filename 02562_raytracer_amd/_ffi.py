@@ -154,6 +154,7 @@ SIGNATURES = {
                                   C.POINTER(RayCounts)]),
     "rt_tileset_local_tiles": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
     "rt_unpack_tiles": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]),
+    "rt_trace_rays": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp]),
     "rt_last_counts": (C.c_int, [vp, C.POINTER(RayCounts)]),
     "rt_selftest_math": (C.c_int, [vp, C.c_uint32, C.c_float, C.c_float, u32p]),
     "rt_mesh_load_obj": (C.c_int, [C.c_char_p, C.POINTER(vp)]),

@@ -174,6 +174,11 @@ def make_uniform(eye, target, up, constant, width, height, selection1=0, subdiv=
     return u
 
 
+# include/rt.h rt_ray_hit
+RAY_HIT_DTYPE = np.dtype([("tri", "<u4"), ("dist", "<f4"), ("beta", "<f4"), ("gamma", "<f4"), ("ntested", "<u4"),
+                          ("tested_fnv", "<u4"), ("tmin", "<f4"), ("tmax", "<f4")])
+
+
 class DeviceBuffer:
     """HBM allocation owned by a Context (frame buffers)."""
 
@@ -381,6 +386,31 @@ class Context:
         vpn = (lambda p: C.c_void_p(p) if p else None)
         self._chk(F.lib().rt_unpack_tiles(self._h, width, height, nranks, vpn(packed_accum), vpn(packed_ids),
                                           vpn(frame_accum), vpn(frame_ids)))
+
+    def trace_rays(self, trav, rays, anyhit=None):
+        """rt_trace_rays on host arrays: rays float32[n, 8] (origin, direction,
+        tmin, tmax), anyhit bool[n] or None.  Returns a structured array with the
+        fields of rt_ray_hit (tri, dist, beta, gamma, ntested, tested_fnv, tmin, tmax)."""
+        rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+        n = rays.shape[0]
+        out = np.zeros(n, dtype=RAY_HIT_DTYPE)
+        if n == 0:
+            return out
+        rb = self.alloc(rays.nbytes)
+        hb = self.alloc(out.nbytes)
+        fb = None
+        try:
+            rb.from_numpy(rays)
+            if anyhit is not None:
+                fb = self.alloc(4 * n)
+                fb.from_numpy(np.ascontiguousarray(np.asarray(anyhit).astype(np.uint32)))
+            self._chk(F.lib().rt_trace_rays(self._h, F.TRAVERSALS.get(trav, trav), C.c_void_p(rb.ptr),
+                                            C.c_void_p(fb.ptr) if fb else None, n, C.c_void_p(hb.ptr)))
+            return hb.to_numpy(RAY_HIT_DTYPE, (n,))
+        finally:
+            for b in (rb, hb, fb):
+                if b is not None:
+                    b.free()
 
     def last_counts(self):
         cnt = F.RayCounts()

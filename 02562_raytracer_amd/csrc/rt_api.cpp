@@ -260,7 +260,8 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
         c->waves_per_cu = (int)value;
         return RT_OK;
     case RT_OPT_SHADE_THRESHOLD:
-        if (value < 0 || value > 64) return fail(c, RT_E_INVALID, "shade threshold must be in [0,64] (64 = lockstep)");
+        if (value < -1 || value > 64)
+            return fail(c, RT_E_INVALID, "shade threshold must be in [0,64] (64 = lockstep), or -1 (the default)");
         c->shade_threshold = (int)value;
         return RT_OK;
     case RT_OPT_SAMPLE_CHUNK:
@@ -773,29 +774,9 @@ int rt_set_environment_map(rt_ctx* c, const uint8_t* rgba8, uint32_t width, uint
     return RT_OK;
 }
 
-static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
+// The device-resident scene as the kernels read it (rt_internal.h DevScene).
+static rtk::DevScene dev_scene(const rt_ctx* c)
 {
-    if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
-    if (mode < RT_MODE_W1E6 || mode > RT_MODE_W9E3) return fail(c, RT_E_INVALID, "rt_render: bad mode");
-    // W7E1/W7E2: progressive, folded inside k_direct (no per-iteration samples)
-    const bool direct_prog = mode == RT_MODE_W7E1 || mode == RT_MODE_W7E2;
-    // progressive path tracers: per-iteration samples, folded in order by k_fold
-    const bool path = mode == RT_MODE_W7E3 || mode == RT_MODE_W9E1 || mode == RT_MODE_W8E1 || mode == RT_MODE_W8E2 ||
-                      mode == RT_MODE_W8E3 || mode == RT_MODE_W9E2 || mode == RT_MODE_W9E3;
-    if (mode == RT_MODE_W1E6) {
-        if (trav != RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "W1E6 is analytic: traverse must be NONE");
-    } else {
-        if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_render: no mesh uploaded");
-        if (trav == RT_TRAVERSE_BSP && !c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_render: no BSP uploaded");
-        if (trav == RT_TRAVERSE_BVH && !c->has_bvh) return fail(c, RT_E_NOT_READY, "rt_render: no BVH uploaded");
-        if (trav == RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "mesh modes need BSP or BVH");
-        if (path && mode != RT_MODE_W9E1 && mode != RT_MODE_W9E2 && mode != RT_MODE_W9E3 && c->nlights < 2)
-            return fail(c, RT_E_INVALID, "W7E3/W8 sample area lights: the mesh has no emissive (illum 1) triangle");
-        if ((mode == RT_MODE_W6E1 || mode == RT_MODE_PROJECT) && trav == RT_TRAVERSE_BSP && !c->has_bsp)
-            return fail(c, RT_E_NOT_READY, "rt_render: W6E1/PROJECT need the BSP root AABB");
-    }
-    if (!L.accum) return fail(c, RT_E_INVALID, "rt_render: accum buffer required");
-    if (int r = set_dev(c)) return r;
     rtk::DevScene S;
     memset(&S, 0, sizeof S);
     S.pos = c->pos.as<float4>();
@@ -819,6 +800,55 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     S.bvh_rec_off = c->bvh_rec_off;
     S.bvh_ids = c->bvh_ids.as<uint32_t>();
     S.bvh_nnodes = c->bvh_nnodes;
+    return S;
+}
+
+int rt_trace_rays(rt_ctx* c, rt_traverse trav, const float* rays, const uint32_t* flags, uint32_t n, rt_ray_hit* hits)
+{
+    if (!c) return RT_E_INVALID;
+    if (n == 0) return RT_OK;
+    if (!rays || !hits) return fail(c, RT_E_INVALID, "rt_trace_rays: rays and hits are required");
+    if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_trace_rays: no mesh uploaded");
+    if (trav == RT_TRAVERSE_BSP && !c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_trace_rays: no BSP uploaded");
+    if (trav == RT_TRAVERSE_BVH && !c->has_bvh) return fail(c, RT_E_NOT_READY, "rt_trace_rays: no BVH uploaded");
+    if (trav != RT_TRAVERSE_BSP && trav != RT_TRAVERSE_BVH)
+        return fail(c, RT_E_UNSUPPORTED, "rt_trace_rays: traverse must be BSP or BVH");
+    if (int r = set_dev(c)) return r;
+    uint32_t* deep = nullptr;
+    if (trav == RT_TRAVERSE_BVH) {
+        const size_t need = rtk::bvh_deep_bytes(c->num_cus, 16);
+        if (c->bvh_deep.n < need) HIPCHK(c, c->bvh_deep.alloc(need));
+        deep = c->bvh_deep.as<uint32_t>();
+    }
+    const int r = rtk::launch_query(dev_scene(c), trav, rays, flags, n, hits, deep, c->num_cus, c->stream);
+    if (r) return fail(c, r, std::string("rt_trace_rays: launch failed: ") + hipGetErrorString(hipGetLastError()));
+    return RT_OK;
+}
+
+static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
+{
+    if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
+    if (mode < RT_MODE_W1E6 || mode > RT_MODE_W9E3) return fail(c, RT_E_INVALID, "rt_render: bad mode");
+    // W7E1/W7E2: progressive, folded inside k_direct (no per-iteration samples)
+    const bool direct_prog = mode == RT_MODE_W7E1 || mode == RT_MODE_W7E2;
+    // progressive path tracers: per-iteration samples, folded in order by k_fold
+    const bool path = mode == RT_MODE_W7E3 || mode == RT_MODE_W9E1 || mode == RT_MODE_W8E1 || mode == RT_MODE_W8E2 ||
+                      mode == RT_MODE_W8E3 || mode == RT_MODE_W9E2 || mode == RT_MODE_W9E3;
+    if (mode == RT_MODE_W1E6) {
+        if (trav != RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "W1E6 is analytic: traverse must be NONE");
+    } else {
+        if (!c->has_mesh) return fail(c, RT_E_NOT_READY, "rt_render: no mesh uploaded");
+        if (trav == RT_TRAVERSE_BSP && !c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_render: no BSP uploaded");
+        if (trav == RT_TRAVERSE_BVH && !c->has_bvh) return fail(c, RT_E_NOT_READY, "rt_render: no BVH uploaded");
+        if (trav == RT_TRAVERSE_NONE) return fail(c, RT_E_UNSUPPORTED, "mesh modes need BSP or BVH");
+        if (path && mode != RT_MODE_W9E1 && mode != RT_MODE_W9E2 && mode != RT_MODE_W9E3 && c->nlights < 2)
+            return fail(c, RT_E_INVALID, "W7E3/W8 sample area lights: the mesh has no emissive (illum 1) triangle");
+        if ((mode == RT_MODE_W6E1 || mode == RT_MODE_PROJECT) && trav == RT_TRAVERSE_BSP && !c->has_bsp)
+            return fail(c, RT_E_NOT_READY, "rt_render: W6E1/PROJECT need the BSP root AABB");
+    }
+    if (!L.accum) return fail(c, RT_E_INVALID, "rt_render: accum buffer required");
+    if (int r = set_dev(c)) return r;
+    const rtk::DevScene S = dev_scene(c);
     L.u = c->u;
     rtk::camera_basis(c->u, L.cam);
     L.jitter = c->has_jitter ? c->jitter.as<float>() : nullptr;
@@ -836,8 +866,14 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // BVH 2-4 best, 4695 vs 4604 Mrays/s at 8)
     // defaults per walk and shader (profiles/r02/ab_w7e3_shards.txt: W7E3's short
     // Cornell-box rays shade often, and refilling earlier pays there)
+    // The BSP walk of the other modes chooses per wave between 8 and 32 (bit 16:
+    // adaptive, k_path "Shading threshold"): 8 for walk-dominated scenes (configs
+    // 3, 4), 32 for test-dominated ones (config 5's 32-triangle leaves;
+    // profiles/r02/sweep_T_r2final.txt).
     L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold
-                                   : trav == RT_TRAVERSE_BVH ? 4 : mode == RT_MODE_W7E3 ? 24 : 8);
+                                   : trav == RT_TRAVERSE_BVH ? 4
+                                   : mode == RT_MODE_W7E3    ? 24
+                                                             : (1u << 16) | (32u << 8) | 8u);
     L.reserved0 = 0;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));

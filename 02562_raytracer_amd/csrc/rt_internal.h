@@ -77,6 +77,10 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
 // bytes of the deep BVH stack for a grid of at most num_cus x waves_per_cu waves
 size_t bvh_deep_bytes(int num_cus, int waves_per_cu);
 
+// rt_trace_rays: one walk per ray (k_query); bvh_deep sized bvh_deep_bytes(num_cus, 16)
+int launch_query(const DevScene& s, rt_traverse trav, const float* rays, const uint32_t* flags, uint32_t n,
+                 rt_ray_hit* out, uint32_t* bvh_deep, int num_cus, hipStream_t stream);
+
 // Progressive average of one pass's per-iteration samples into accum/ids (after k_path).
 int launch_fold(const DevLaunch& l, hipStream_t stream);
 

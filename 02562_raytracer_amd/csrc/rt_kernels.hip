@@ -332,6 +332,28 @@ __device__ __forceinline__ void trav_init(Trav& t, float tmin, float tmax)
 }
 __device__ __forceinline__ TraceOut trav_out(const Trav& t) { return TraceOut{t.hit_k, t.beta, t.gamma, t.tmax}; }
 
+// ------------------------------------------------------------------ tested-triangle log
+// The walks report each triangle they test (its record's byte offset) to a LOG:
+// NoLog (every render kernel) compiles to nothing; the ray-query kernel
+// (k_query) hashes the tested ids in order (FNV-1a over little-endian u32, as
+// tests/golden/gen_js_walk.js hashes the reference walk's tests).
+struct NoLog {
+    __device__ __forceinline__ void tested(uint32_t) {}
+};
+struct FnvLog {
+    const uint32_t* ids;   // record slot -> triangle id (treeIds / bvh_triangles)
+    uint32_t rec_off;      // byte offset of record slot 0 in the walk's buffer
+    uint32_t n, h, last;
+    __device__ __forceinline__ void tested(uint32_t k)
+    {
+        const uint32_t id = ids[(k - rec_off) / 48u];
+#pragma unroll
+        for (int b = 0; b < 4; b++) h = (h ^ ((id >> (8 * b)) & 0xFFu)) * 0x01000193u;
+        n++;
+        last = id;
+    }
+};
+
 // ------------------------------------------------------------------ BSP traversal
 // intersect_trimesh, bsp.wgsl:10-81, as a per-lane state machine: each call
 // visits at most one node and tests at most one triangle ("if-if"), so a wave
@@ -435,13 +457,14 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 #ifndef RT_LEAF_TESTS
 #define RT_LEAF_TESTS 2   // triangle tests per leaf trip of the BSP walk: 1 or 2
 #endif
-template <bool COUNT, bool CULL>
+template <bool COUNT, bool CULL, class LOG>
 __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const f3 o, const f3 d,
-                                               bool anyhit, Trav& t, Counters& c)
+                                               bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
     if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
         const v4u r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 16u, 0, 0);
         const v4u r2 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
+        lg.tested(t.leaf_k);
         if (COUNT) {
             c.v[C_IDS]++;
             c.v[C_TESTS]++;
@@ -463,11 +486,12 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
 
 // The leaf half of a BSP trip: test the record in q0..q2 (and, with
 // RT_LEAF_TESTS 2, the next one, whose first 16 B are q3).
-template <bool COUNT, bool CULL>
+template <bool COUNT, bool CULL, class LOG>
 __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, const v4u q0, const v4u q1, const v4u q2,
                                                const v4u q3, const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c,
-                                               bool& done, bool& pop)
+                                               bool& done, bool& pop, LOG& lg)
 {
+    lg.tested(t.leaf_k);
     if (COUNT) {
         c.v[C_IDS]++;
         c.v[C_TESTS]++;
@@ -482,7 +506,7 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
         t.gamma = anyhit ? t.gamma : gamma;
     }
     t.leaf_k += 48u;
-    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c);
+    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c, lg);
     const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
     done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
     pop = leaf_done & !t.found;
@@ -524,9 +548,9 @@ __device__ __forceinline__ bool bsp_walk(float* stk, const v4u q0, const v4u q1,
     return leaf & !pop;
 }
 
-template <bool COUNT, bool CULL = false>
-__device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
-                                         bool anyhit, Trav& t, Counters& c)
+template <bool COUNT, bool CULL, class LOG>
+__device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
+                                             bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
@@ -546,10 +570,17 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
             c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
     }
     bool done = false, pop = false;
-    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, o, d, anyhit, t, c, done, pop);
+    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, o, d, anyhit, t, c, done, pop, lg);
     else bsp_walk<COUNT>(stk, q0, q1, q2, q3, o, d, inv, t, c, pop);
     if (pop) done = bsp_pop(stk, t);
     return done;
+}
+template <bool COUNT, bool CULL = false>
+__device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
+                                         bool anyhit, Trav& t, Counters& c)
+{
+    NoLog lg;
+    return bsp_step_log<COUNT, CULL>(S, stk, o, d, inv, anyhit, t, c, lg);
 }
 
 // RN(1/denom) per axis (denom as bsp.wgsl:63): the approximate interior-node
@@ -667,9 +698,9 @@ __device__ __forceinline__ uint32_t bvh_slot(uint32_t i) { return i < 50u ? i : 
 // {min.xyz, w0}{max.xyz, w1}, interior w0 = byte offset of the right child
 // (the left child is the next record), w1 = 0; leaf w0 = byte offset of its
 // first triangle record, w1 = 48 * n_prims.
-template <bool COUNT, bool CULL = false>
-__device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const BvhDeep& dp, const f3 o, const f3 d,
-                                         const f3 inv, bool anyhit, Trav& t, Counters& c)
+template <bool COUNT, bool CULL, class LOG>
+__device__ __forceinline__ bool bvh_step_log(const DevScene& S, uint32_t* stk, const BvhDeep& dp, const f3 o,
+                                             const f3 d, const f3 inv, bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bvh_base, (short)0, (int)S.bvh_bytes, 0x00020000);
@@ -692,6 +723,7 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2));
 #endif
     if (in_leaf) {
+        lg.tested(t.leaf_k);
         if (COUNT) {
             c.v[C_IDS]++;
             c.v[C_TESTS]++;
@@ -774,6 +806,13 @@ __device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const
 #endif
     }
     return (t.leaf_k == t.leaf_end) & ((t.lvl >= 1000u) | (t.node == 0u));
+}
+template <bool COUNT, bool CULL = false>
+__device__ __forceinline__ bool bvh_step(const DevScene& S, uint32_t* stk, const BvhDeep& dp, const f3 o, const f3 d,
+                                         const f3 inv, bool anyhit, Trav& t, Counters& c)
+{
+    NoLog lg;
+    return bvh_step_log<COUNT, CULL>(S, stk, dp, o, d, inv, anyhit, t, c, lg);
 }
 
 // The 1/d of bvh.wgsl:155 (exact division: it feeds the slab test directly).
@@ -1226,6 +1265,15 @@ k_path(DevScene S, DevLaunch L)
         cnt.v[C_PRIMARY]++;
     };
 
+    // Shading threshold.  L.shade_threshold bit 16 set: chosen by the wave
+    // between T_lo (bits 0-7) and T_hi (bits 8-15) from the share of its
+    // tracing lanes that sit in a leaf (testing triangles), counted at every
+    // check.  A test-dominated walk (long leaves: config 5's 32-triangle
+    // leaves, 0.83 of the tracing lanes in a leaf) has long, uneven per-lane
+    // tails, so finished lanes are refilled early (T_hi); a walk-dominated one
+    // (config 3: 0.27, config 4: 0.56) keeps the refills together (T_lo) for
+    // the coherence of the pixel-major units.
+    int32_t leaf_score = 0;   // sum of 4 * leaf lanes - 3 * tracing lanes over the checks (wave-uniform)
     uint64_t tstamp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
         // ---- traversal phase: every tracing lane advances its ray by one node
@@ -1233,7 +1281,14 @@ k_path(DevScene S, DevLaunch L)
         for (;;) {
             const uint64_t trm = __ballot(st == ST_TRACE);
             const uint64_t wtm = __ballot(st == ST_SHADE);
-            if (!(trm != 0 && (wtm == 0 || T >= 64u || (uint32_t)__popcll(trm) > T))) break;
+            uint32_t Te = T & 0xFFu;
+            if (TRAV == RT_TRAVERSE_BSP && (T >> 16)) {   // (the host asks for it on the BSP walk only)
+                const int32_t lf = __popcll(__ballot((st == ST_TRACE) & (tr.leaf_k != tr.leaf_end)));
+                leaf_score += 4 * lf - 3 * (int32_t)__popcll(trm);
+                leaf_score = leaf_score < -(1 << 24) ? -(1 << 24) : leaf_score > (1 << 24) ? (1 << 24) : leaf_score;
+                Te = leaf_score >= 0 ? (T >> 8) & 0xFFu : T & 0xFFu;
+            }
+            if (!(trm != 0 && (wtm == 0 || Te >= 64u || (uint32_t)__popcll(trm) > Te))) break;
             if (COUNT) {
                 const bool leafst = tr.leaf_k != tr.leaf_end;
                 const uint64_t nm = __ballot(st == ST_TRACE && !leafst);
@@ -1811,6 +1866,57 @@ __global__ void __launch_bounds__(256) k_primary(DevScene S, DevLaunch L, int pr
         }
     }
     flush_counters(cnt, L.counters, COUNT);
+}
+
+// ------------------------------------------------------------------ ray queries
+// rt_trace_rays: one walk per ray with the render kernels' own step functions
+// (bsp_step / bvh_step): intersect_trimesh (bsp.wgsl:10-81) or intersect_bvh
+// (bvh.wgsl:154-191) for a closest-hit ray, the any-hit walk of the shadow
+// rays (flags bit 0; bsp.wgsl:83-155 stops at the first accept) otherwise.
+// One ray per lane, grid-stride; the tested triangles are hashed in order.
+template <int TRAV>
+__global__ void __launch_bounds__(256) k_query(DevScene S, const float* rays, const uint32_t* flags, uint32_t n,
+                                               rt_ray_hit* out, uint32_t* bvh_deep)
+{
+    extern __shared__ uint32_t lds_stack[];
+    void* stk = TRAV == RT_TRAVERSE_BVH ? lds_stack + (__builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u)
+                                        : lds_stack + threadIdx.x;
+    const BvhDeep dp{TRAV == RT_TRAVERSE_BVH ? bvh_deep + (size_t)blockIdx.x * 256u + threadIdx.x : nullptr,
+                     gridDim.x * 256u};
+    Counters cnt;
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; __ballot(i < n); i += gridDim.x * 256u) {
+        if (i >= n) continue;   // lanes past the end idle (the walk's LDS columns are per lane)
+        const float* r = rays + 8 * (size_t)i;
+        const f3 o = V(r[0], r[1], r[2]), d = V(r[3], r[4], r[5]);
+        const bool anyhit = flags && (flags[i] & 1u);
+        FnvLog lg{TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids,
+                  TRAV == RT_TRAVERSE_BVH ? S.bvh_rec_off : S.bsp_rec_off, 0u, 0x811c9dc5u, 0xFFFFFFFFu};
+        Trav t;
+        t.hit_k = 0;
+        t.beta = t.gamma = 0.0f;
+        trav_start<TRAV>(t, stk, r[6], r[7]);
+        const f3 inv = trav_inv<TRAV>(d);
+        for (uint32_t guard = 0; guard < (1u << 24); guard++) {
+            const bool done = TRAV == RT_TRAVERSE_BVH
+                                  ? bvh_step_log<false, false>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv,
+                                                               anyhit, t, cnt, lg)
+                                  : bsp_step_log<false, false>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t,
+                                                               cnt, lg);
+            if (done) break;
+        }
+        rt_ray_hit h;
+        // an any-hit walk keeps no hit record: its accept is the last tested triangle
+        const uint32_t slot = (t.hit_k - (TRAV == RT_TRAVERSE_BVH ? S.bvh_rec_off : S.bsp_rec_off)) / 48u;
+        h.tri = !t.found ? 0xFFFFFFFFu : anyhit ? lg.last : (TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids)[slot];
+        h.dist = t.found ? t.tmax : 0.0f;
+        h.beta = t.found && !anyhit ? t.beta : 0.0f;
+        h.gamma = t.found && !anyhit ? t.gamma : 0.0f;
+        h.ntested = lg.n;
+        h.tested_fnv = lg.h;
+        h.tmin = t.tmin;
+        h.tmax = t.tmax;
+        out[i] = h;
+    }
 }
 
 // ------------------------------------------------------------------ W6E2 / W7E1 / W7E2 kernel
@@ -2395,6 +2501,24 @@ int launch_render(const DevScene& s, const DevLaunch& l, rt_mode mode, rt_traver
     default:
         return RT_E_UNSUPPORTED;
     }
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+
+int launch_query(const DevScene& s, rt_traverse trav, const float* rays, const uint32_t* flags, uint32_t n,
+                 rt_ray_hit* out, uint32_t* bvh_deep, int num_cus, hipStream_t stream)
+{
+    const size_t lds = trav == RT_TRAVERSE_BVH ? (size_t)RT_BVH_LDS_ENTRIES * 256 * 4
+                                               : (size_t)(s.bsp_depth ? s.bsp_depth : 1) * 256 * 4;
+    uint32_t blocks = (n + 255u) / 256u;
+    const uint32_t cap = (uint32_t)grid_for(num_cus, 16);
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return 0;
+    if (trav == RT_TRAVERSE_BVH)
+        hipLaunchKernelGGL(k_query<RT_TRAVERSE_BVH>, dim3(blocks), dim3(256), lds, stream, s, rays, flags, n, out,
+                           bvh_deep);
+    else
+        hipLaunchKernelGGL(k_query<RT_TRAVERSE_BSP>, dim3(blocks), dim3(256), lds, stream, s, rays, flags, n, out,
+                           bvh_deep);
     return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }
 

@@ -104,11 +104,11 @@ def roofline(key, kern_ms, alg_bytes, config, kernel):
     VALU wave-instructions) come from the committed PMC summary of the same
     workload (profiles/pmc_summary.json, tools/pmc_summary.py; its `source` names
     the rocprofv3 passes); the time is this run's HIP-event kernel time.
-      * config 5 (10M triangles, 1.5 GB of BSP: the scene does not fit in
-        cache): bound "hbm", frac = counter HBM bytes / time / 8 TB/s;
-      * configs 2-4 (cache-resident scenes): bound "valu-issue", frac = VALU
-        wave-instructions / time / the chip's VALU issue rate -- the limit the
-        counters show (DESIGN.md "What bounds it"); the HBM fraction is given beside.
+      * hbm: counter HBM bytes / time / 8 TB/s;
+      * valu-issue: VALU wave-instructions / time / the chip's VALU issue rate;
+      * salu-issue: SALU instructions / time / the probe-measured SALU ceiling.
+    `bound` is whichever of these is largest for this launch (DESIGN.md "What
+    bounds it"); all three are given.
     The SURVEY 8(d) algorithmic bytes (reference layout) over the kernel time is a
     diagnostic ("algorithmic"): the bytes stay in L2/MALL, so against HBM it can
     exceed 1 and is never reported as the HBM fraction."""
@@ -138,10 +138,15 @@ def roofline(key, kern_ms, alg_bytes, config, kernel):
                            "peak_source": "measured ceiling, tools/probes/issue_probe.hip"}
     r["pmc"] = {k: pmc[k] for k in ("source", "kernel_ms_profiled", "l2_hit_rate", "valu_lane_util", "wait_frac",
                                     "write_bytes_per_launch", "fetch_bytes_per_launch") if k in pmc}
-    prim = r["hbm"] if config == 5 else r["valu_issue"]
-    r.update({"bound": "hbm" if config == 5 else "valu-issue", "achieved": prim["achieved"], "peak": prim["peak"],
-              "unit": prim["unit"], "frac": prim["frac"]})
-    if max(r["hbm"]["frac"], r["valu_issue"]["frac"], r.get("salu_issue", {}).get("frac", 0.0)) > 1.0:
+    # the bound is the limit the counters put closest to its peak, whatever the config
+    fr = {"hbm": r["hbm"], "valu-issue": r["valu_issue"]}
+    if "salu_issue" in r:
+        fr["salu-issue"] = r["salu_issue"]
+    bound = max(fr, key=lambda k: fr[k]["frac"])
+    prim = fr[bound]
+    r.update({"bound": bound, "achieved": prim["achieved"], "peak": prim["peak"], "unit": prim["unit"],
+              "frac": prim["frac"]})
+    if max(v["frac"] for v in fr.values()) > 1.0:
         # a summary of another kernel build
         r.update({"bound": "unmeasured", "frac": None, "note": f"PMC summary for {key} does not match this kernel"})
     return r
@@ -176,6 +181,9 @@ def main():
     ap.add_argument("--unit-order", type=int, default=None)
     ap.add_argument("--dump-frame", default=None,
                     help="rank 0 saves the last step's assembled frame (accum + ids) to this .npz")
+    ap.add_argument("--rank-share", type=int, default=None,
+                    help="profiling: one process renders only rank 0's share of an N-rank split (the work one GPU "
+                         "of the N-GPU bench does); its roofline is looked up under the _nN PMC key")
     args = ap.parse_args()
 
     import torch
@@ -184,6 +192,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # launched by torch.distributed.run (the driver's N-GPU form): the process
+    # group and the gather to rank 0 run for any N, so `--nproc-per-node 1`
+    # executes the RCCL path on one GPU
+    use_dist = world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+    share = args.rank_share or 1   # tile split: world ranks, or rank 0 of a --rank-share split
+    if args.rank_share and use_dist:
+        raise SystemExit("--rank-share is a single-process profiling mode")
+    nsplit = world if use_dist else share
     # rehearsal knob: RT_BENCH_DEVICE pins every rank to one device (N ranks
     # sharing a single GPU exercise the N>1 path where only one GPU exists)
     if os.environ.get("RT_BENCH_DEVICE") is not None:
@@ -191,7 +207,7 @@ def main():
     # RCCL (backend "nccl"); RT_BENCH_DIST_BACKEND=gloo is the rehearsal path
     # with RT_BENCH_DEVICE (RCCL refuses two ranks on one GPU): host gathers
     backend = os.environ.get("RT_BENCH_DIST_BACKEND", "nccl")
-    if world > 1:
+    if use_dist:
         torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -235,11 +251,11 @@ def main():
     ctx.set_uniforms(rt.make_uniform(*cam, W, H, selection1=0))
     setup_s = time.perf_counter() - t0
 
-    lt = rt.local_tiles(W, H, world)
+    lt = rt.local_tiles(W, H, nsplit)
     acc_local = torch.empty((lt * 64, 4), dtype=torch.float32, device=dev)
     ids_local = torch.empty((lt * 64,), dtype=torch.int32, device=dev)
     acc_all = ids_all = None
-    if world > 1 and rank == 0:   # gather-to-root: only rank 0 receives the packed tiles
+    if use_dist and rank == 0:   # gather-to-root: only rank 0 receives the packed tiles
         acc_all = torch.empty((world * lt * 64, 4), dtype=torch.float32, device=dev)
         ids_all = torch.empty((world * lt * 64,), dtype=torch.int32, device=dev)
     frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
@@ -248,14 +264,16 @@ def main():
     def step(events=None):
         if events is not None:
             events[0].record(stream)
-        ctx.render_tiles(wl.mode, trav, rank, world, 0, spp, acc_local.data_ptr(), ids_local.data_ptr())
+        ctx.render_tiles(wl.mode, trav, rank, nsplit, 0, spp, acc_local.data_ptr(), ids_local.data_ptr())
         if events is not None:
             events[1].record(stream)
-        if world > 1:
+        if use_dist:
             tiling.gather_tiles(dist, acc_local, ids_local, acc_all, ids_all)
             if rank == 0:
                 ctx.unpack_tiles(W, H, world, acc_all.data_ptr(), ids_all.data_ptr(), frame.data_ptr(),
                                  frame_ids.data_ptr())
+        elif share > 1:
+            pass   # rank 0's share alone: no frame to assemble
         else:
             ctx.unpack_tiles(W, H, 1, acc_local.data_ptr(), ids_local.data_ptr(), frame.data_ptr(),
                              frame_ids.data_ptr())
@@ -274,7 +292,7 @@ def main():
     rays = torch.tensor([counts["primary"] + counts["shadow"], counts["primary"], counts["shadow"],
                          counts["bounce"], algorithmic_bytes(detail, trav)],
                         dtype=torch.float64, device=dev)
-    if world > 1:
+    if use_dist:
         rays = all_reduce(dist, rays, dist.ReduceOp.SUM)
     rays = rays.cpu().numpy()
 
@@ -283,14 +301,14 @@ def main():
     # step's other kernels -- fold, unpack -- and the gather are excluded)
     ctx.set_option(rt._ffi.RT_OPT_KERNEL_TIMING, 1)
     ctx.kernel_time(reset=True)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize(dev)
-    if world > 1:
+    if use_dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_total, launches = ctx.kernel_time(reset=True)
@@ -298,21 +316,25 @@ def main():
     launches_per_step = launches // args.steps
     kern_ms = kern_total / max(1, launches)   # average k_path launch
     render_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    kern_ms_own = kern_ms   # this rank's own launches: the roofline pairs them with this rank's counters
     t = torch.tensor([elapsed, kern_ms, render_ms], dtype=torch.float64, device=dev)
-    if world > 1:
+    if use_dist:
         t = all_reduce(dist, t, dist.ReduceOp.MAX)
     elapsed, kern_ms, render_ms = [float(x) for x in t.cpu().numpy()]
 
     value = rays[0] * args.steps / elapsed / 1e6
     if rank == 0:
-        # roofline of the dominant kernel (k_path<mode, traversal>): one launch on one GPU
-        bytes_per_launch = rays[4] / world / max(1, launches_per_step)
-        roof = roofline(pmc_key(W, H, spp, trav, world, args.config), kern_ms, bytes_per_launch, args.config,
+        # roofline of the dominant kernel (k_path<mode, traversal>): one launch on
+        # one GPU -- rank 0's, with rank 0's own kernel time and the PMC summary of
+        # rank 0's share (profiles/pmc_summary.json key _n<N>, measured with --rank-share N)
+        bytes_per_launch = rays[4] / (world if use_dist else 1) / max(1, launches_per_step)
+        roof = roofline(pmc_key(W, H, spp, trav, nsplit, args.config), kern_ms_own, bytes_per_launch, args.config,
                         f"k_path<{wl.mode},{trav}>")
         roof["launches_per_step"] = launches_per_step
         roof["render_ms"] = round(render_ms, 3)
+        roof["kernel_ms_max_over_ranks"] = round(kern_ms, 3)
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline and not use_dist and share == 1:
             cpu = cpu_baseline(wl, trav, mesh, accel, spp, W, H, args.cpu_budget)
         line = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world, "steps": args.steps,
@@ -321,9 +343,11 @@ def main():
             "config": {"workload": f"config {wl.number}: {wl.name} ({mesh.ntris} tris), "
                                    f"{trav}{' D20/leaf4' if trav == 'BSP' else ' leaf4'}, {W}x{H}, {spp} spp/step",
                        "resolution": [W, H], "spp": spp, "traversal": trav, "ntris": mesh.ntris, "mode": wl.mode,
-                       "parallelism": f"tiles8x8/{world}",
-                       "world_size": dist.get_world_size() if world > 1 else 1,
-                       "backend": dist.get_backend() if world > 1 else None},
+                       "parallelism": f"tiles8x8/{nsplit}",
+                       "world_size": dist.get_world_size() if use_dist else 1,
+                       "backend": dist.get_backend() if use_dist else None,
+                       **({"share": f"rank 0 of {share} (profiling: this GPU's part of the {share}-GPU frame)"}
+                          if share > 1 else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
             "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},
@@ -340,7 +364,7 @@ def main():
         if args.dump_frame:
             np.savez(args.dump_frame, accum=frame.cpu().numpy(), ids=frame_ids.cpu().numpy().view(np.uint32))
     ctx.close()
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

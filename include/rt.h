@@ -160,7 +160,7 @@ typedef struct rt_ray_counts {
 /* ---- options (rt_set_option) ------------------------------------------- */
 #define RT_OPT_DETAIL_COUNTERS 1  /* 0/1: use the counting kernel instantiation    */
 #define RT_OPT_WAVES_PER_CU    2  /* persistent grid size: waves per CU (default 32; capped by LDS) */
-#define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace (default: 8 for the BSP walk, 24 for W7E3 on it, 4 for the BVH walk); 0 or 64 = all lanes finish their rays first (lockstep) */
+#define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace; 0 or 64 = all lanes finish their rays first (lockstep); -1 = the default: 24 for W7E3 on the BSP walk, 4 for the BVH walk, and for the other modes on the BSP walk a per-wave choice of 8 or 32 from the share of its tracing lanes inside a leaf (32 when >= 3/4) */
 #define RT_OPT_SAMPLE_CHUNK    4  /* W7E3/W9E1: progressive iterations per work unit (default 1) */
 #define RT_OPT_SAMPLE_BUDGET_MB 5 /* W7E3/W9E1: device scratch for per-sample results, MiB (default 16384);
                                      a render whose spp x pixels x 16 B exceed it runs in several passes */
@@ -357,6 +357,30 @@ int rt_frame_rgba8(rt_ctx* ctx, const float* accum_rgba32f, uint32_t npix, uint8
 int rt_unpack_tiles(rt_ctx* ctx, uint32_t width, uint32_t height, uint32_t nranks,
                     const float* packed_accum, const uint32_t* packed_ids,
                     float* frame_accum, uint32_t* frame_ids);
+
+/* ---- ray queries: the walk alone ------------------------------------------ */
+
+/* One walk per ray through the context's BSP or BVH, with the render kernels'
+ * own traversal step: intersect_trimesh (res/shaders/bsp.wgsl:10-81) /
+ * intersect_bvh (bvh.wgsl:154-191) for a closest-hit ray; with bit 0 of
+ * flags[i] set, the any-hit walk of the shadow and occlusion rays (it stops at
+ * the first accepted triangle, as intersect_trimesh_immediate_return,
+ * bsp.wgsl:83-155, does).  The query form of the reference's CPU walk
+ * intersect_bsp_array (js/bsp_tree/modules/BspTree_interleaved.js:287-352).
+ *   rays:  DEVICE, n x 8 floats: origin.xyz, direction.xyz, tmin, tmax;
+ *   flags: DEVICE, n u32, or NULL (all closest-hit);
+ *   hits:  DEVICE, n x rt_ray_hit.
+ * Asynchronous on the context stream. */
+typedef struct rt_ray_hit {
+    uint32_t tri;          /* the accepted triangle (the last accept), UINT32_MAX on a miss */
+    float dist;            /* its distance (the ray's tmax when the walk ends) */
+    float beta, gamma;     /* its barycentrics (0 for an any-hit walk, which keeps none) */
+    uint32_t ntested;      /* triangles tested, in walk order */
+    uint32_t tested_fnv;   /* FNV-1a 32 of the tested triangle ids (little-endian u32) in order */
+    float tmin, tmax;      /* the ray interval the walk leaves behind (bsp.wgsl narrows it in place) */
+} rt_ray_hit;
+int rt_trace_rays(rt_ctx* ctx, rt_traverse trav, const float* rays, const uint32_t* flags, uint32_t n,
+                  rt_ray_hit* hits);
 
 /* Counters of the most recent launch (synchronizes). */
 int rt_last_counts(rt_ctx* ctx, rt_ray_counts* counts);

@@ -150,6 +150,11 @@ void or_camera_ray(const or_uniform* u, uint32_t x, uint32_t y, float jx, float 
  * Returns -1 when the clip rejects the ray, else hit (1) / miss (0); reports
  * the ray interval the walk leaves behind (bsp.wgsl mutates it in place) and
  * the triangle ids in the order they were tested (up to cap; *ntested = all). */
+/* or_render on one thread, logging every traced ray (8 floats: origin, direction,
+ * tmin, tmax) in trace order into rays[cap]; *nrays = rays traced (may exceed cap) */
+int or_render_raylog(const or_scene* s, const or_uniform* u, int mode, int trav, uint32_t x0, uint32_t y0, uint32_t w,
+                     uint32_t h, uint32_t first_iter, uint32_t spp, float* accum, uint32_t* ids, float* rays,
+                     uint32_t cap, uint32_t* nrays);
 int or_trace_query(const or_scene* s, int trav, int clip, const float o[3], const float d[3], float tmin,
                    float tmax, uint32_t* tri, float* dist, float* out_tmin, float* out_tmax, uint32_t* tested,
                    uint32_t cap, uint32_t* ntested);

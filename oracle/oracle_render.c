@@ -61,6 +61,8 @@ typedef struct {
     or_counts c;
     uint32_t* log;       /* or_trace_query: triangle ids in test order (NULL: off) */
     uint32_t log_cap, log_n;
+    float* rlog;         /* or_render_raylog: every traced ray, 8 floats (NULL: off) */
+    uint32_t rlog_cap, rlog_n;
 } Ctx;
 
 /* ------------------------------------------------------------ PRNG (w7e3.wgsl:141-172) */
@@ -259,6 +261,15 @@ static int trace_bvh(Ctx* C, Ray* r, Hit* h, int face_normals)
 
 static int trace(Ctx* C, Ray* r, Hit* h, int face_normals)
 {
+    if (C->rlog) {   /* or_render_raylog: the ray as the walk receives it */
+        if (C->rlog_n < C->rlog_cap) {
+            float* q = C->rlog + 8 * (size_t)C->rlog_n;
+            q[0] = r->origin.x; q[1] = r->origin.y; q[2] = r->origin.z;
+            q[3] = r->direction.x; q[4] = r->direction.y; q[5] = r->direction.z;
+            q[6] = r->tmin; q[7] = r->tmax;
+        }
+        C->rlog_n++;
+    }
     return C->trav == OR_TRAV_BVH ? trace_bvh(C, r, h, face_normals) : trace_bsp(C, r, h, face_normals);
 }
 
@@ -1402,6 +1413,8 @@ typedef struct {
     volatile uint32_t next_row;
     pthread_mutex_t mu;
     or_counts total;
+    float* rlog;         /* single-threaded ray log (or_render_raylog) */
+    uint32_t rlog_cap, rlog_n;
 } Job;
 
 static void render_row(Job* J, Ctx* C, const Cam* cam, uint32_t ry)
@@ -1456,12 +1469,15 @@ static void* worker(void* arg)
     C.jitter = J->jitter;
     C.mode = J->mode;
     C.trav = J->trav;
+    C.rlog = J->rlog;
+    C.rlog_cap = J->rlog_cap;
     Cam cam = make_cam(J->u);
     for (;;) {
         uint32_t ry = __sync_fetch_and_add(&J->next_row, 1u);
         if (ry >= J->h) break;
         render_row(J, &C, &cam, ry);
     }
+    J->rlog_n = C.rlog_n;
     pthread_mutex_lock(&J->mu);
     uint64_t* d = (uint64_t*)&J->total;
     const uint64_t* sC = (const uint64_t*)&C.c;
@@ -1470,9 +1486,33 @@ static void* worker(void* arg)
     return NULL;
 }
 
+static int render_job(const or_scene* s, const or_uniform* u, const float* jitter, int mode, int trav,
+                      uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
+                      float* accum, uint32_t* ids, or_counts* counts, int nthreads, float* rlog, uint32_t rlog_cap,
+                      uint32_t* rlog_n);
+
 int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int mode, int trav,
               uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
               float* accum, uint32_t* ids, or_counts* counts, int nthreads)
+{
+    return render_job(s, u, jitter, mode, trav, x0, y0, w, h, first_iter, spp, accum, ids, counts, nthreads, NULL, 0,
+                      NULL);
+}
+
+/* or_render on one thread, logging every ray trace() receives (origin,
+ * direction, tmin, tmax) in trace order: the primary, shadow and bounce rays
+ * of the shaders as the walk sees them (tests/golden/gen_js_walk2.py) */
+int or_render_raylog(const or_scene* s, const or_uniform* u, int mode, int trav, uint32_t x0, uint32_t y0, uint32_t w,
+                     uint32_t h, uint32_t first_iter, uint32_t spp, float* accum, uint32_t* ids, float* rays,
+                     uint32_t cap, uint32_t* nrays)
+{
+    return render_job(s, u, NULL, mode, trav, x0, y0, w, h, first_iter, spp, accum, ids, NULL, 1, rays, cap, nrays);
+}
+
+static int render_job(const or_scene* s, const or_uniform* u, const float* jitter, int mode, int trav,
+                      uint32_t x0, uint32_t y0, uint32_t w, uint32_t h, uint32_t first_iter, uint32_t spp,
+                      float* accum, uint32_t* ids, or_counts* counts, int nthreads, float* rlog, uint32_t rlog_cap,
+                      uint32_t* rlog_n)
 {
     if (mode < 0 || mode > OR_MODE_W9E3) return -1;
     if (mode != OR_MODE_W1E6) {
@@ -1488,7 +1528,9 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
     J.s = s; J.u = u; J.jitter = jitter; J.mode = mode; J.trav = trav;
     J.x0 = x0; J.y0 = y0; J.w = w; J.h = h; J.first_iter = first_iter; J.spp = spp;
     J.accum = accum; J.ids = ids;
+    J.rlog = rlog; J.rlog_cap = rlog_cap;
     pthread_mutex_init(&J.mu, NULL);
+    if (rlog) nthreads = 1;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     pthread_t th[256];
@@ -1497,6 +1539,7 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
     for (int i = 1; i < nthreads; i++) pthread_join(th[i], NULL);
     pthread_mutex_destroy(&J.mu);
     if (counts) *counts = J.total;
+    if (rlog_n) *rlog_n = J.rlog_n;
     return 0;
 }
 

@@ -15,8 +15,9 @@
 //     OBJParser_interleaved.js getDrawingInfo, filled from the mesh the caller
 //     passes (the reference loader's triangles, tests/golden/gen_js_walk.py).
 // Instrumentation: intersect_triangle is wrapped (the walk calls the global by
-// name) to log the tested triangle ids in order and to record the id of the last
-// accepted one -- the walk itself runs unmodified.
+// name) to log the tested triangle ids in order, to record the id of the last
+// accepted one and where the first accept came (the prefix an any-hit walk tests)
+// -- the walk itself runs unmodified.
 // usage: node gen_js_walk.js <reference js/bsp_tree/modules dir> <in.json> <out.json>
 'use strict';
 const fs = require('fs');
@@ -57,11 +58,13 @@ vm.runInContext('build_bsp_tree(g_drawingInfo, __device, {})', Object.assign(san
 
 vm.runInContext(`
 var __log = [];
+var __first = -1;   // tests up to and including the first accept (the any-hit walk's prefix)
 const __intersect_triangle = intersect_triangle;
 intersect_triangle = function (r, hit, idx) {
   __log.push(idx);
   const ok = __intersect_triangle(r, hit, idx);
   if (ok) hit.tri = idx;
+  if (ok && __first < 0) __first = __log.length;
   return ok;
 };
 `, sandbox);
@@ -75,16 +78,18 @@ const query = vm.runInContext(`(function (o, d, tmin, tmax, clip) {
   const ray = { origin: [o[0], o[1], o[2]], direction: [d[0], d[1], d[2]], tmin: tmin, tmax: tmax };
   const hit = { has_hit: false, dist: 0.0, tri: -1 };
   __log = [];
+  __first = -1;
   let status;
   if (clip && !intersect_min_max(ray)) status = -1;
   else status = intersect_bsp_array(ray, hit) ? 1 : 0;
-  return [status, hit.tri, hit.dist, ray.tmin, ray.tmax, __log.slice()];
+  return [status, hit.tri, hit.dist, ray.tmin, ray.tmax, __log.slice(), __first];
 })`, sandbox);
 
 const results = [];
 for (const r of inp.rays) {
-  const [st, tri, dist, t0, t1, log] = query(r[0], r[1], r[2], r[3], r[4]);
-  results.push([st, tri, dist, t0, t1, log.length, fnv(log)]);
+  const [st, tri, dist, t0, t1, log, first] = query(r[0], r[1], r[2], r[3], r[4]);
+  const pre = first < 0 ? log : log.slice(0, first);
+  results.push([st, tri, dist, t0, t1, log.length, fnv(log), pre.length, fnv(pre)]);
 }
 const tree = vm.runInContext('({ tree: bspTree, planes: bspPlanes, ids: treeIds })', sandbox);
 const sha = crypto.createHash('sha256');

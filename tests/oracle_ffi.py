@@ -103,6 +103,9 @@ def lib():
         L.or_trace_query.argtypes = [C.POINTER(Scene), C.c_int, C.c_int, f32p, f32p, C.c_float, C.c_float,
                                      u32p, f32p, f32p, f32p, u32p, C.c_uint32, u32p]
         L.or_trace_brute.argtypes = [C.POINTER(Scene), f32p, f32p, C.c_float, C.c_float, u32p, f32p]
+        L.or_render_raylog.argtypes = [C.POINTER(Scene), C.POINTER(Uniform), C.c_int, C.c_int, C.c_uint32,
+                                       C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32, f32p, u32p, f32p,
+                                       C.c_uint32, u32p]
         for n in ("or_det_sinf", "or_det_cosf", "or_det_acosf"):
             getattr(L, n).argtypes = [C.c_float]
             getattr(L, n).restype = C.c_float
@@ -278,6 +281,23 @@ def render(scene, uniform, mode, trav, region, first_iter=0, spp=1, accum=None, 
     if rc != 0:
         raise ValueError(f"or_render = {rc}")
     return accum, ids, cnt.asdict()
+
+
+def render_raylog(scene, uniform, mode, trav, region, first_iter=0, spp=1, cap=1 << 20):
+    """render() on one thread that also returns every ray the walk received, in
+    trace order: float32[n, 8] = origin, direction, tmin, tmax."""
+    L = lib()
+    x0, y0, w, h = region
+    accum = np.zeros((h, w, 4), dtype=np.float32)
+    ids = np.zeros((h, w), dtype=np.uint32)
+    rays = np.zeros((cap, 8), dtype=np.float32)
+    n = C.c_uint32()
+    rc = L.or_render_raylog(C.byref(scene.s), C.byref(uniform), MODES[mode], TRAVS[trav], x0, y0, w, h, first_iter,
+                            spp, accum.ctypes.data_as(f32p), ids.ctypes.data_as(u32p), rays.ctypes.data_as(f32p), cap,
+                            C.byref(n))
+    if rc != 0 or n.value > cap:
+        raise ValueError(f"or_render_raylog = {rc}, {n.value} rays")
+    return accum, ids, rays[:n.value].copy()
 
 
 def trace_one(scene, trav, o, d, tmin, tmax, face_normals=1):

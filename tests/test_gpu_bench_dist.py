@@ -29,15 +29,15 @@ def _port():
         return s.getsockname()[1]
 
 
-def _bench(nproc, out):
+def _bench(nproc, out, launcher=None, backend="gloo"):
     args = ["bench.py", "--gpus", str(nproc), "--steps", "1", "--warmup", "1", "--config", "2", "--spp", str(SPP),
             "--width", str(W), "--height", str(H), "--no-cpu-baseline", "--dump-frame", out]
-    if nproc > 1:
+    if nproc > 1 if launcher is None else launcher:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
                "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
     else:
         cmd = [sys.executable] + args
-    env = dict(os.environ, RT_BENCH_DEVICE="0", RT_BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    env = dict(os.environ, RT_BENCH_DEVICE="0", RT_BENCH_DIST_BACKEND=backend, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
@@ -72,3 +72,36 @@ def test_eight_rank_bench_frame_equals_one_rank(tmp_path):
     assert eight["rays_per_step"] == one["rays_per_step"]
     assert np.array_equal(f1["ids"], f8["ids"])
     assert np.array_equal(f1["accum"].view(np.uint32), f8["accum"].view(np.uint32))
+
+
+def test_one_rank_rccl_bench_frame_equals_plain_run(tmp_path):
+    # the driver's launch form with one process: torch.distributed.run opens an
+    # RCCL ("nccl") process group on device 0 (bench.py init_process_group with
+    # device_id), the packed tiles go through tiling.gather_tiles' nccl branch
+    # (dist.gather of device tensors) and rt_unpack_tiles; the counters and times
+    # go through RCCL all_reduce.  The frame equals the plain 1-process run's.
+    one, f1 = _bench(1, str(tmp_path / "n1.npz"))
+    nc, fn = _bench(1, str(tmp_path / "nccl1.npz"), launcher=True, backend="nccl")
+    assert nc["config"]["backend"] == "nccl" and nc["config"]["world_size"] == 1
+    assert one["config"]["backend"] is None
+    assert nc["rays_per_step"] == one["rays_per_step"]
+    assert np.array_equal(f1["ids"], fn["ids"])
+    assert np.array_equal(f1["accum"].view(np.uint32), fn["accum"].view(np.uint32))
+
+
+def test_rank_share_renders_rank0_tiles(tmp_path):
+    # --rank-share N: one process renders rank 0's share of an N-rank split (the
+    # profiling form of one GPU's work in the N-GPU bench); its rays are rank 0's
+    # part of the 1-rank total
+    one, _ = _bench(1, str(tmp_path / "n1.npz"))
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--config", "2", "--spp",
+                        str(SPP), "--width", str(W), "--height", str(H), "--no-cpu-baseline", "--rank-share", "4"],
+                       cwd=ROOT, env=dict(os.environ, OMP_NUM_THREADS="2"), capture_output=True, text=True,
+                       timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    assert line["config"]["parallelism"] == "tiles8x8/4" and "share" in line["config"]
+    assert 0 < line["rays_per_step"]["primary"] < one["rays_per_step"]["primary"]
+    # 25 x 17 = 425 whole tiles (200 and 136 are multiples of 8); rank 0 of 4
+    # holds tiles 0, 4, ..., 424: 107 tiles, one primary ray per pixel-iteration
+    assert line["rays_per_step"]["primary"] == 107 * 64 * SPP

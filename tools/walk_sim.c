@@ -1,0 +1,171 @@
+/* walk_sim.c -- trip-count model of k_path's BSP walk,
+ * for pricing walk changes on the CPU before building them.  Test/tool code:
+ * not part of the product.
+ *
+ * Replays bsp.wgsl:10-81 (the oracle's trace_bsp) per ray in f32 and counts
+ * the trips the kernel's per-lane state machine needs (bsp_step: a walking
+ * trip reads one 64-B treelet and decides up to three levels; a leaf trip
+ * tests up to two triangles; an empty leaf or a leaf without a hit pops at
+ * the end of its trip), under variants of the walk:
+ *   v0  the committed walk;
+ *   v1  + "skip empty near child": a push whose near child is an empty leaf
+ *       would pop straight back (tmin = t, tmax unchanged, node = far), so the
+ *       walk goes to the far child at once, in the same trip;
+ *   v2  + "skip empty far child": a pending entry whose far child is an empty
+ *       leaf is popped past (its pop would only reach that leaf and pop again),
+ *       in the same trip as the pop that reaches it.
+ * All variants return the same hit (checked per ray against v0).
+ * Build: gcc -O2 -ffp-contract=off -shared -fPIC -o walk_sim.so walk_sim.c */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+typedef struct { float x, y, z; } v3;
+static v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
+static v3 sub(v3 a, v3 b) { return V(a.x - b.x, a.y - b.y, a.z - b.z); }
+static float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static v3 cross(v3 a, v3 b) { return V(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+static float comp(v3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+typedef struct {
+    const uint32_t* tree;   /* nnodes x 4 (reference layout, 0-based, children 2i+1, 2i+2) */
+    const float* planes;
+    const uint32_t* ids;
+    const float* pos;       /* float4 */
+    const uint32_t* idx;    /* uint4 */
+} Scene;
+
+static int tri(const Scene* s, uint32_t v, v3 o, v3 w, float tmin, float tmax, float* dist)
+{
+    const uint32_t* ix = s->idx + 4 * (size_t)v;
+    v3 v0 = V(s->pos[4 * ix[0]], s->pos[4 * ix[0] + 1], s->pos[4 * ix[0] + 2]);
+    v3 v1 = V(s->pos[4 * ix[1]], s->pos[4 * ix[1] + 1], s->pos[4 * ix[1] + 2]);
+    v3 v2 = V(s->pos[4 * ix[2]], s->pos[4 * ix[2] + 1], s->pos[4 * ix[2] + 2]);
+    v3 e0 = sub(v1, v0), e1 = sub(v2, v0), ov = sub(v0, o);
+    v3 n = cross(e0, e1), nom = cross(ov, w);
+    float den = dot(w, n);
+    if (fabsf(den) < 1e-10f) return 0;
+    float b = dot(nom, e1) / den, g = -dot(nom, e0) / den, d = dot(ov, n) / den;
+    if (b < 0.0f || g < 0.0f || b + g > 1.0f || d > tmax || d < tmin) return 0;
+    *dist = d;
+    return 1;
+}
+
+static int is_empty_leaf(const Scene* s, uint32_t node) { return (s->tree[4 * node] & 3u) == 3u && (s->tree[4 * node] >> 2) == 0; }
+static uint32_t depth_of(uint32_t n0) { uint32_t m = n0 + 1, d = 0; while (m > 1) { m >>= 1; d++; } return d; }
+
+/* stats[variant][k]: 0 walk trips, 1 leaf trips, 2 interior decisions, 3 leaf visits,
+ * 4 empty leaf visits, 5 tests, 6 pushes, 7 pops, 8 hits, 9 mismatches vs v0 */
+enum { S_WT, S_LT, S_DEC, S_LEAF, S_EMPTY, S_TEST, S_PUSH, S_POP, S_HIT, S_BAD, S_N };
+
+static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int anyhit, float* hd, uint32_t* htri,
+                double* st)
+{
+    uint32_t stk_node[64], stk_dep[64], stk_skip[64];
+    float stk_t[64], stk_tmax[64];
+    int sp = 0;
+    uint32_t node = 0;
+    int found = 0;
+    for (;;) {
+        /* one walking trip from `node`: up to three levels */
+        st[S_WT] += 1;
+        int lv = 0, reached_leaf = 0, do_pop = 0;
+        while (lv < 3) {
+            const uint32_t* tn = s->tree + 4 * (size_t)node;
+            uint32_t ax = tn[0] & 3u;
+            if (ax == 3u) {
+                st[S_LEAF] += 1;
+                uint32_t cnt = tn[0] >> 2, first = tn[1];
+                if (cnt == 0) {
+                    st[S_EMPTY] += 1;
+                    do_pop = 1;
+                } else {
+                    /* leaf trips: two tests per trip */
+                    uint32_t j = 0;
+                    while (j < cnt) {
+                        st[S_LT] += 1;
+                        for (int k = 0; k < 2 && j < cnt; k++, j++) {
+                            float dd;
+                            st[S_TEST] += 1;
+                            if (tri(s, s->ids[first + j], o, d, tmin, tmax, &dd)) {
+                                tmax = dd;
+                                *hd = dd;
+                                *htri = s->ids[first + j];
+                                found = 1;
+                                if (anyhit) { j = cnt; break; }
+                            }
+                        }
+                    }
+                    if (found) { st[S_HIT] += 1; return 1; }
+                    do_pop = 1;
+                }
+                reached_leaf = 1;
+                break;
+            }
+            st[S_DEC] += 1;
+            float ad = comp(d, (int)ax), ao = comp(o, (int)ax);
+            uint32_t nearn = ad >= 0.0f ? tn[2] : tn[3], farn = ad >= 0.0f ? tn[3] : tn[2];
+            float den = fabsf(ad) < 1.0e-8f ? 1.0e-8f : ad;
+            float t = (s->planes[node] - ao) / den;
+            if (t > tmax) {
+                node = nearn;
+            } else if (t < tmin) {
+                node = farn;
+            } else if (var >= 1 && is_empty_leaf(s, nearn)) {
+                /* push + visit the empty near leaf + pop, folded: the counted
+                 * leaf visit and pop of v0 are skipped */
+                tmin = t;
+                node = farn;
+            } else {
+                st[S_PUSH] += 1;
+                stk_node[sp] = farn;
+                stk_dep[sp] = depth_of(node);
+                stk_skip[sp] = var >= 2 && is_empty_leaf(s, farn);
+                stk_t[sp] = t;
+                stk_tmax[sp] = tmax;
+                sp++;
+                tmax = t;
+                node = nearn;
+            }
+            lv++;
+        }
+        if (!reached_leaf && !do_pop) continue;   /* next trip from the node three levels down */
+        if (do_pop) {
+            /* pop (v2: past entries whose far child is an empty leaf) */
+            for (;;) {
+                if (sp == 0) return 0;
+                sp--;
+                st[S_POP] += 1;
+                node = stk_node[sp];
+                tmin = stk_t[sp];
+                tmax = stk_tmax[sp];
+                if (!stk_skip[sp]) break;
+                st[S_LEAF] += 1;   /* the reference visits that empty leaf */
+                st[S_EMPTY] += 1;
+            }
+        }
+    }
+}
+
+/* rays: n x 8 floats (o.xyz, d.xyz, tmin, tmax), flags: n (bit 0 anyhit).
+ * out: 3 x S_N doubles (per variant) */
+int walk_sim(const uint32_t* tree, const float* planes, const uint32_t* ids, const float* pos, const uint32_t* idx,
+             const float* rays, const uint32_t* flags, uint32_t n, double* out)
+{
+    Scene s = {tree, planes, ids, pos, idx};
+    memset(out, 0, sizeof(double) * 3 * S_N);
+    for (uint32_t i = 0; i < n; i++) {
+        const float* r = rays + 8 * (size_t)i;
+        v3 o = V(r[0], r[1], r[2]), d = V(r[3], r[4], r[5]);
+        float h0 = -1, hv;
+        uint32_t t0 = ~0u, tv;
+        int f0 = walk(&s, 0, o, d, r[6], r[7], flags[i] & 1, &h0, &t0, out);
+        for (int v = 1; v < 3; v++) {
+            hv = -1;
+            tv = ~0u;
+            int fv = walk(&s, v, o, d, r[6], r[7], flags[i] & 1, &hv, &tv, out + v * S_N);
+            if (fv != f0 || (f0 && (hv != h0 || tv != t0))) out[v * S_N + S_BAD] += 1;
+        }
+    }
+    return 0;
+}

@@ -1,0 +1,87 @@
+"""Trip-count model of k_path's BSP walk under walk variants (tools/walk_sim.c).
+Rays: camera rays of a workload (random pixels, jittered), the W9E1 shadow ray
+of every hit (any-hit, direction (0, 1, 0), [1e-4, 999999 - 1e-4]) and a
+cosine bounce about the face normal.  usage: python tools/walk_sim.py [config] [rays]"""
+import ctypes
+import os
+import subprocess
+import sys
+import time
+from importlib import import_module
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import oracle_ffi as O  # noqa: E402
+
+NAMES = ["walk_trips", "leaf_trips", "decisions", "leaf_visits", "empty_leaves", "tests", "pushes", "pops", "hits",
+         "mismatch"]
+
+
+def lib():
+    src = os.path.join(ROOT, "tools", "walk_sim.c")
+    so = "/tmp/walk_sim.so"
+    if not os.path.exists(so) or os.path.getmtime(so) < os.path.getmtime(src):
+        subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-shared", "-fPIC", "-o", so, src], check=True)
+    return ctypes.CDLL(so)
+
+
+def main():
+    cfgn = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    nr = int(sys.argv[2]) if len(sys.argv) > 2 else 20000
+    cfg = import_module("02562_raytracer_amd.configs").WORKLOADS[cfgn]
+    mesh = cfg.mesh()
+    tree, planes, ids, aabb, D = mesh.bsp_tree(20, 4).arrays()
+    pos, nrm, idx, mats, lights = mesh.arrays()
+    import types
+    m = types.SimpleNamespace(pos=pos, nrm=nrm, idx=idx, ntris=idx.shape[0], mats=np.ascontiguousarray(mats),
+                              lights=lights)
+    b = types.SimpleNamespace(aabb=aabb, tree=tree, planes=planes, ids=ids, max_depth=D)
+    sc = O.SceneRef(m, b)
+    u = O.make_uniform(*cfg.camera, cfg.width, cfg.height)
+    rng = np.random.default_rng(1)
+    rays, flags = [], []
+    t0 = time.time()
+    for _ in range(nr):
+        x, y = int(rng.integers(cfg.width)), int(rng.integers(cfg.height))
+        o, d = O.camera_ray(u, x, y, float(rng.random()) / cfg.height, float(rng.random()) / cfg.height)
+        rays.append([*o, *d, 1e-4, 5000.0])
+        flags.append(0)
+        hit, tri, dist = O.trace_one(sc, "BSP", o, d, 1e-4, 5000.0)
+        if hit:
+            p = (o + d * np.float32(dist)).astype(np.float32)
+            rays.append([*p, 0.0, 1.0, 0.0, 1e-4, np.float32(999999.0) - np.float32(1e-4)])
+            flags.append(1)
+            v0, v1, v2 = (pos[idx[tri, k], :3] for k in range(3))
+            n = np.cross(v1 - v0, v2 - v0)
+            n = n / np.linalg.norm(n)
+            if np.dot(n, d) > 0:
+                n = -n
+            a = rng.normal(size=3)
+            a = a - n * np.dot(a, n)
+            a /= np.linalg.norm(a)
+            c = np.sqrt(rng.random())
+            w = (n * np.sqrt(1 - c * c) + a * c).astype(np.float32)
+            rays.append([*p, *w, 1e-4, 5000.0])
+            flags.append(0)
+    R = np.ascontiguousarray(np.array(rays, np.float32))
+    F = np.ascontiguousarray(np.array(flags, np.uint32))
+    out = np.zeros(30, np.float64)
+    L = lib()
+    P = ctypes.c_void_p
+    L.walk_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
+               P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
+               P(out.ctypes.data))
+    out = out.reshape(3, 10)
+    print(f"config {cfgn}: {len(R)} rays ({sum(flags)} any-hit), {time.time() - t0:.1f} s")
+    for v in range(3):
+        s = {k: round(out[v, i] / len(R), 3) for i, k in enumerate(NAMES)}
+        s["mismatch"] = int(out[v, 9])
+        tr = out[v, 0] + out[v, 1]
+        print(f"v{v}", s, "trips/ray", round(tr / len(R), 3), "vs v0", round(tr / (out[0, 0] + out[0, 1]), 4))
+
+
+if __name__ == "__main__":
+    main()
