@@ -1,23 +1,31 @@
 // rt_kernels.hip -- gfx950 (CDNA4) kernels for the per-pixel traversal + shading
 // hot path of cakarsubasi/02562_raytracer (res/shaders/*.wgsl).
 //
-// Structure (DESIGN.md "Kernels"):
-//   * persistent grid (num_CUs x waves_per_CU waves): pixel slots come from a
-//     global atomic queue in 8x8-tile order, one atomic per wave refill, slots
-//     handed to the idle lanes with ballot + mbcnt (active-lane compaction);
-//   * one lane = one pixel, running all `spp` progressive iterations of that
-//     pixel in order (accumulation is sequential per pixel, w7e3.wgsl:261-271);
-//   * ray state machine with ONE traversal call site: each loop trip every
-//     tracing lane advances its current ray (camera / bounce closest-hit, or a
-//     shadow any-hit) by at most one node and one triangle ("if-if"); lanes
-//     whose ray ended shade and start their next ray once few enough lanes
-//     are still tracing (shade_threshold), so no lane idles behind the
-//     slowest ray of its wave;
-//   * per-lane traversal stack in LDS, [level][thread] layout (conflict-free):
-//     BSP: a bit trail in a register + 4-B t per depth (MAX_LEVEL entries);
-//     BVH: 4-B node indices x 50;
-//   * BSP nodes packed to 8 B (children implicit), triangles pre-transformed to
-//     48-B records {v0, e0, e1, n} in treeIds order (one 3 x dwordx4 gather).
+// Structure of the path tracers' k_path:
+//   * persistent grid (num_CUs x waves_per_CU waves, capped by LDS and by the
+//     register budget) over WORK UNITS of one (pixel, iteration) pair: the
+//     iterations of a pixel are independent (the PRNG seed is tea16(pixel,
+//     iteration)), so a unit traces one sample and writes its radiance and
+//     primary-hit id as a 16-B record to samples[pixel][iteration];
+//   * k_fold then applies the progressive average of w7e3.wgsl:261-271 to every
+//     pixel in iteration order -- bit-identical to the reference's spp
+//     sequential render() calls;
+//   * units come from 8 work shards, one per XCD (HW_REG_XCC_ID), each owning
+//     every 8th block of 64 consecutive units, with its queue head in its own
+//     128-B line; a wave refill is one atomic, and ballot + mbcnt hand the
+//     slots to the idle lanes (active-lane compaction); pixel-major unit order
+//     gives a refill's lanes the iterations of one pixel (coherent rays);
+//   * ray state machine with ONE traversal call site: each trip every tracing
+//     lane advances its ray (camera / bounce closest-hit, or a shadow any-hit)
+//     by one 64-B load: a treelet walked three BSP levels deep, or a leaf's
+//     triangle records (two tests per trip); lanes whose ray ended wait and
+//     shade together once few lanes still trace (shading threshold, chosen
+//     per wave from its leaf share), so no lane waits for the slowest ray;
+//   * per-lane traversal stack in LDS, [level][thread] (conflict-free):
+//     BSP: a bit trail in a register + one 4-B tmax per depth;
+//     BVH: 16 entries in LDS, the rest of the 50 in a per-lane global region;
+//   * BSP treelets and triangle records ({v0, e0, e1, n}, 48 B, in treeIds
+//     order) share one buffer resource; out-of-range reads return 0.
 // Numerics: -ffp-contract=off, correctly rounded f32 div/sqrt, pinned
 // transcendentals (include/rt_detmath.h) => bit-identical to the CPU oracle.
 #include <type_traits>
@@ -268,7 +276,15 @@ __device__ __forceinline__ void pixel_uv(const rt_uniform& u, uint32_t x, uint32
 // bsp_decide).
 // CULL: the back-face culling test of w9e3.wgsl:328 (|denom| < 5e-5 or
 // denom > 0 rejects) in place of |denom| < 1e-10.
-template <bool FAST, bool COUNT = false, bool CULL = false>
+// BARY false (the walks' trip loops with RT_LAZY_BARY): the barycentrics are
+// not returned, and a candidate whose approximate quotients already settle
+// every condition of the accept predicate (beta and gamma non-negative by the
+// sign of a*r and b*r, their sum below 1 and the distance inside [tmin, tmax]
+// by the same margins as the rejections) is accepted after dividing out only
+// dist, which becomes tmax; beta and gamma are derived where the hit is shaded
+// (bary_of: the same operations on the same record, so the same bits).  Only
+// an unsettled candidate divides all three quotients.
+template <bool FAST, bool COUNT = false, bool CULL = false, bool BARY = true>
 __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const float4 r2, f3 o, f3 w, float tmin,
                                          float tmax, float& dist, float& beta, float& gamma, Counters* cn = nullptr)
 {
@@ -281,25 +297,60 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
     const float b = -dot(nom, e0);
     const float c = dot(ov, n);
     bool reject = CULL ? ((rt_absf(denom) < 0.00005f) | (denom > 0.0f)) : rt_absf(denom) < 1e-10f;
+    float tq = 0.0f, m = 0.0f, qa = 0.0f, qb = 0.0f, ms = 0.0f;
+    bool inr = false;
     if (FAST) {
         // certain rejections, each implying the exact predicate below rejects:
         // a sign (beta < 0 / gamma < 0), the distance range, or
         // RN(beta + gamma) > 1 (needs beta + gamma > 1 + 2^-24: margin 2^-22)
         const float r = __builtin_amdgcn_rcpf(denom);
-        const float tq = c * r;
-        const float m = __builtin_fmaf(rt_absf(tq), 0x1p-20f, 1e-30f);   // the product is exact: = mul + add
-        const float qa = a * r, qb = b * r;
-        const float ms = (rt_absf(qa) + rt_absf(qb)) * 0x1p-20f;
-        reject = reject | ((rt_absf(denom) <= 0x1p60f) & ((qa < -0x1p-100f) | (qb < -0x1p-100f) |
-                                                          (tq - m > tmax) | (tq + m < tmin) |
-                                                          (qa + qb - ms > 1.0f + 0x1p-22f)));
+        tq = c * r;
+        m = __builtin_fmaf(rt_absf(tq), 0x1p-20f, 1e-30f);   // the product is exact: = mul + add
+        qa = a * r;
+        qb = b * r;
+        ms = (rt_absf(qa) + rt_absf(qb)) * 0x1p-20f;
+        inr = rt_absf(denom) <= 0x1p60f;
+        reject = reject | (inr & ((qa < -0x1p-100f) | (qb < -0x1p-100f) | (tq - m > tmax) | (tq + m < tmin) |
+                                  (qa + qb - ms > 1.0f + 0x1p-22f)));
     }
     if (reject) return false;
     if (COUNT) cn->v[C_EXACT_TESTS]++;
+    dist = c / denom;
+    if (FAST && !BARY) {
+        // certain accepts (decided only for the candidates that survive): the
+        // sign of a*r is the sign of a/denom (so a clear sign bit means
+        // RN(a/denom) is +0 or positive, never < 0); the sum and the range with
+        // the margins above, on the other side
+        const bool sure = inr & !(__float_as_uint(qa) >> 31) & !(__float_as_uint(qb) >> 31) &
+                          (qa + qb + ms < 1.0f - 0x1p-22f) & (tq - m >= tmin) & (tq + m <= tmax);
+        if (sure) return true;
+    }
     beta = a / denom;
     gamma = b / denom;
-    dist = c / denom;
     return !((beta < 0.0f) | (gamma < 0.0f) | (beta + gamma > 1.0f) | (dist > tmax) | (dist < tmin));
+}
+#ifndef RT_LAZY_BARY
+#define RT_LAZY_BARY 1
+#endif
+// beta and gamma of the accepted record at byte offset k of the walk's buffer
+// for the ray (o, w): intersect_triangle's a / denom and b / denom with the
+// operations of tri_math (the trip loop does not keep them, RT_LAZY_BARY)
+template <int TRAV>
+__device__ __forceinline__ void bary_of(const DevScene& S, uint32_t k, const f3 o, const f3 w, float& beta,
+                                        float& gamma)
+{
+    const uint8_t* base = TRAV == RT_TRAVERSE_BVH ? S.bvh_base : reinterpret_cast<const uint8_t*>(S.bsp_nodes);
+    const float4* rp = reinterpret_cast<const float4*>(base + k);
+    const float4 r0 = rp[0], r1 = rp[1], r2 = rp[2];
+    const f3 v0 = V(r0.x, r0.y, r0.z), e0 = V(r0.w, r1.x, r1.y), e1 = V(r1.z, r1.w, r2.x);
+    const f3 n = V(r2.y, r2.z, r2.w);
+    const f3 ov = sub(v0, o);
+    const f3 nom = cross(ov, w);
+    const float denom = dot(w, n);
+    const float a = dot(nom, e1);
+    const float b = -dot(nom, e0);
+    beta = a / denom;
+    gamma = b / denom;
 }
 struct TraceOut {
     uint32_t k;   // record slot of the accepted triangle
@@ -398,6 +449,12 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 // stores the current tmax into the depth-dep slot unconditionally: no pending
 // entry lives at a depth >= depth(m) (they are all ancestors of m), so the
 // store is dead unless the trail bit is set.
+// RT_TRAIL_SLOT 1: the walk derives the trail slot of its first level once per
+// trip and the next levels' slots as constant offsets from it (ds_write
+// immediate offsets), and sets the trail bit with one shift-or.
+#ifndef RT_TRAIL_SLOT
+#define RT_TRAIL_SLOT 1
+#endif
 template <bool COUNT>
 __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, uint32_t dep, const f3 o,
                                                const f3 d, const f3 inv, Trav& t, Counters& c)
@@ -426,8 +483,13 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     const bool inside = amb & !(tt > t.tmax);
     const bool gofar = cfar | (inside & (tt < t.tmin));
     const bool push = inside & !(tt < t.tmin);
-    stk[dep * 256u] = t.tmax;   // the tmax its pop restores
-    t.lvl |= push ? 1u << dep : 0u;
+    if (RT_TRAIL_SLOT) {
+        stk[0] = t.tmax;   // stk: this level's slot (bsp_walk)
+        t.lvl |= (uint32_t)push << dep;
+    } else {
+        stk[dep * 256u] = t.tmax;   // the tmax its pop restores
+        t.lvl |= push ? 1u << dep : 0u;
+    }
     t.tmax = push ? tt : t.tmax;
     return gofar ? near_node ^ 1u : near_node;
 }
@@ -470,15 +532,18 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
             c.v[C_TESTS]++;
         }
         float dist, beta, gamma;
-        if (tri_math<true, COUNT, CULL>(as_f4(nx), as_f4(r1), as_f4(r2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+        if (tri_math<true, COUNT, CULL, !RT_LAZY_BARY>(as_f4(nx), as_f4(r1), as_f4(r2), o, d, t.tmin, t.tmax, dist,
+                                                       beta, gamma, &c)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
             // an any-hit walk keeps the hit it started from (k_path redraws from
             // it); selects, not a branch (no exec-mask work in the trip)
             t.hit_k = anyhit ? t.hit_k : t.leaf_k;
-            t.beta = anyhit ? t.beta : beta;
-            t.gamma = anyhit ? t.gamma : gamma;
+            if (!RT_LAZY_BARY) {
+                t.beta = anyhit ? t.beta : beta;
+                t.gamma = anyhit ? t.gamma : gamma;
+            }
         }
         t.leaf_k += 48u;
     }
@@ -497,13 +562,16 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
         c.v[C_TESTS]++;
     }
     float dist, beta, gamma;
-    if (tri_math<true, COUNT, CULL>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+    if (tri_math<true, COUNT, CULL, !RT_LAZY_BARY>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta,
+                                                   gamma, &c)) {
         if (COUNT) c.v[C_ACCEPTS]++;
         t.tmax = dist;
         t.found = true;
         t.hit_k = anyhit ? t.hit_k : t.leaf_k;
-        t.beta = anyhit ? t.beta : beta;
-        t.gamma = anyhit ? t.gamma : gamma;
+        if (!RT_LAZY_BARY) {
+            t.beta = anyhit ? t.beta : beta;
+            t.gamma = anyhit ? t.gamma : gamma;
+        }
     }
     t.leaf_k += 48u;
     if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c, lg);
@@ -527,15 +595,17 @@ __device__ __forceinline__ bool bsp_walk(float* stk, const v4u q0, const v4u q1,
     uint2 n = make_uint2(q0.x, q0.y);
     bool leaf = (n.x & 3u) == 3u;
     if (!leaf) {
-        m = bsp_decide<COUNT>(stk, n, m, dep, o, d, inv, t, c);
+        // the trail slot of this level (RT_TRAIL_SLOT), or the trail base
+        float* const s0 = RT_TRAIL_SLOT ? stk + dep * 256u : stk;
+        m = bsp_decide<COUNT>(s0, n, m, dep, o, d, inv, t, c);
         n = (m & 1u) ? make_uint2(q1.x, q1.y) : make_uint2(q0.z, q0.w);
         leaf = (n.x & 3u) == 3u;
         if (!leaf) {
-            m = bsp_decide<COUNT>(stk, n, m, dep + 1u, o, d, inv, t, c);
+            m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 256 : stk, n, m, dep + 1u, o, d, inv, t, c);
             const v4u g = (m & 2u) ? q3 : q2;
             n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
             leaf = (n.x & 3u) == 3u;
-            if (!leaf) m = bsp_decide<COUNT>(stk, n, m, dep + 2u, o, d, inv, t, c);
+            if (!leaf) m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 512 : stk, n, m, dep + 2u, o, d, inv, t, c);
         }
     }
     t.node = m;
@@ -730,15 +800,18 @@ __device__ __forceinline__ bool bvh_step_log(const DevScene& S, uint32_t* stk, c
         }
         float dist, beta, gamma;
         // the BVH walk never narrows the ray interval: both bounds are exact
-        if (tri_math<true, COUNT, CULL>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta, gamma, &c)) {
+        if (tri_math<true, COUNT, CULL, !RT_LAZY_BARY>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist,
+                                                       beta, gamma, &c)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
             // an any-hit walk keeps the hit it started from (k_path redraws from
             // it); selects, not a branch (no exec-mask work in the trip)
             t.hit_k = anyhit ? t.hit_k : t.leaf_k;
-            t.beta = anyhit ? t.beta : beta;
-            t.gamma = anyhit ? t.gamma : gamma;
+            if (!RT_LAZY_BARY) {
+                t.beta = anyhit ? t.beta : beta;
+                t.gamma = anyhit ? t.gamma : gamma;
+            }
         }
         t.leaf_k += 48u;
         if (anyhit & t.found) return true;
@@ -850,6 +923,7 @@ __device__ __forceinline__ bool trace(const DevScene& S, void* stk, const BvhDee
     const f3 inv = trav_inv<TRAV>(d);
     for (uint32_t guard = 0; guard < (1u << 24); guard++)
         if (trav_step<TRAV, COUNT>(S, stk, dp, o, d, inv, anyhit, t, c)) break;
+    if (RT_LAZY_BARY && t.found && !anyhit) bary_of<TRAV>(S, t.hit_k, o, d, t.beta, t.gamma);
     out = trav_out(t);
     return t.found;
 }
@@ -954,12 +1028,14 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 
 // ------------------------------------------------------------------ W7E3 / W9E1 path kernel
 // Persistent "while-while" megakernel with per-lane work regeneration:
-//   * every lane owns one pixel and runs its `spp` iterations in order; a lane
-//     whose pixel is finished takes the next pixel slot from the global queue
-//     (wave-aggregated: one atomic per refill, slots handed out with
+//   * a lane owns one work unit at a time -- one iteration of one pixel (or
+//     RT_OPT_SAMPLE_CHUNK consecutive ones) -- and writes that iteration's
+//     16-B sample record; an idle lane takes the next unit from its XCD's work
+//     shard (wave-aggregated: one atomic per refill, slots handed out with
 //     ballot + mbcnt prefix ranks, so idle lanes are compacted onto new work);
 //   * traversal phase: each loop trip advances every tracing lane by one BSP
-//     node / BVH pop; lanes whose ray finished wait;
+//     treelet (three levels) or two triangle tests / one BVH pop; lanes whose
+//     ray finished wait;
 //   * shading phase: entered when at most `shade_threshold` lanes are still
 //     tracing (or none): the finished lanes shade, set up their next ray
 //     (shadow, bounce or the next sample) and rejoin; lanes still mid-ray keep
@@ -1343,6 +1419,8 @@ k_path(DevScene S, DevLaunch L)
             bool sample_done = false;
             if (!shadow) {
                 if (tr.found) {
+                    // the hit's barycentrics, kept in tr across a shadow walk (REDRAW)
+                    if (RT_LAZY_BARY) bary_of<TRAV>(S, tr.hit_k, ro, rd, tr.beta, tr.gamma);
                     const HitRec h = resolve<TRAV, W9E3>(S, trav_out(tr), ro, rd, !W9);
                     if (bounce == 0) prim = h.tri;
                     const rt_material& m = mat_of(S, h.material);
@@ -1909,6 +1987,7 @@ __global__ void __launch_bounds__(256) k_query(DevScene S, const float* rays, co
         const uint32_t slot = (t.hit_k - (TRAV == RT_TRAVERSE_BVH ? S.bvh_rec_off : S.bsp_rec_off)) / 48u;
         h.tri = !t.found ? 0xFFFFFFFFu : anyhit ? lg.last : (TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids)[slot];
         h.dist = t.found ? t.tmax : 0.0f;
+        if (RT_LAZY_BARY && t.found && !anyhit) bary_of<TRAV>(S, t.hit_k, o, d, t.beta, t.gamma);
         h.beta = t.found && !anyhit ? t.beta : 0.0f;
         h.gamma = t.found && !anyhit ? t.gamma : 0.0f;
         h.ntested = lg.n;

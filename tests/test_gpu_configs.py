@@ -76,6 +76,20 @@ def test_config4_bunny_grid_region(rt, gpu, configs):
     s.ctx.close()
 
 
+def test_config4_baseline_spp_region(rt, gpu, configs):
+    # config 4's BASELINE 256 spp, in one launch, on a 32x32 region where the
+    # grid's bunnies overlap on screen (long, bouncing paths)
+    wl = configs[4]
+    assert wl.spp == 256
+    s = Scene(rt, wl.mesh(), wl.traversal, env=wl.env, oracle_accel_from_product=True)
+    region = (944, 500, 32, 32)
+    g = s.render_gpu(wl.mode, wl.camera, wl.width, wl.height, region, 0, wl.spp)
+    o = s.render_oracle(wl.mode, wl.camera, wl.width, wl.height, region, 0, wl.spp)
+    check(g, o)
+    assert g[2]["samples"] == 32 * 32 * wl.spp and g[2]["bounce"] > 0
+    s.ctx.close()
+
+
 @pytest.mark.parametrize("trav", ["BSP", "BVH"])
 def test_config5_soup_region(rt, gpu, configs, trav):
     wl = configs[5]

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--trav", default=None)
     ap.add_argument("--chunks", default="1")   # the bench's one-iteration units
+    ap.add_argument("--warm", type=int, default=1, help="untimed render of every share before timing it (0: only "
+                    "one warm-up render, for the long configs 4 and 5)")
     args = ap.parse_args()
     import torch
     rt = importlib.import_module("02562_raytracer_amd")
@@ -47,6 +49,11 @@ def main():
 def probe(ctx, rt, wl, trav, W, H, spp, dev, stream, args, chunk):
     import torch
     out = {}
+    if not args.warm:   # one warm-up launch for the whole probe
+        lt = rt.local_tiles(W, H, 8)
+        acc = torch.empty((lt * 64, 4), dtype=torch.float32, device=dev)
+        ctx.render_tiles(wl.mode, trav, 0, 8, 0, min(spp, 4), acc.data_ptr(), None)
+        torch.cuda.synchronize(dev)
     for n in [int(x) for x in args.ns.split(",")]:
         lt = rt.local_tiles(W, H, n)
         acc = torch.empty((lt * 64, 4), dtype=torch.float32, device=dev)
@@ -54,13 +61,15 @@ def probe(ctx, rt, wl, trav, W, H, spp, dev, stream, args, chunk):
         ms = []
         for r in range(n):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            ctx.render_tiles(wl.mode, trav, r, n, 0, spp, acc.data_ptr(), ids.data_ptr())   # warm
+            if args.warm:
+                ctx.render_tiles(wl.mode, trav, r, n, 0, spp, acc.data_ptr(), ids.data_ptr())   # warm
             e0.record(stream)
             ctx.render_tiles(wl.mode, trav, r, n, 0, spp, acc.data_ptr(), ids.data_ptr())
             e1.record(stream)
             torch.cuda.synchronize(dev)
             ms.append(e0.elapsed_time(e1))
-        out[n] = {"max_ms": round(max(ms), 3), "mean_ms": round(sum(ms) / n, 3)}
+        out[n] = {"max_ms": round(max(ms), 3), "mean_ms": round(sum(ms) / n, 3),
+                  "rank_ms": [round(x, 3) for x in ms]}
         print(json.dumps({"chunk": chunk, "n": n, **out[n]}), flush=True)
     t1 = out[min(out)]["max_ms"]
     print(json.dumps({"chunk": chunk, "projected_speedup": {n: round(t1 / v["max_ms"], 2) for n, v in out.items()}}))

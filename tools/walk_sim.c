@@ -51,6 +51,8 @@ static int tri(const Scene* s, uint32_t v, v3 o, v3 w, float tmin, float tmax, f
     return 1;
 }
 
+int g_levels = 3;
+void walk_sim_levels(int l) { g_levels = l; }
 static int is_empty_leaf(const Scene* s, uint32_t node) { return (s->tree[4 * node] & 3u) == 3u && (s->tree[4 * node] >> 2) == 0; }
 static uint32_t depth_of(uint32_t n0) { uint32_t m = n0 + 1, d = 0; while (m > 1) { m >>= 1; d++; } return d; }
 
@@ -70,7 +72,7 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
         /* one walking trip from `node`: up to three levels */
         st[S_WT] += 1;
         int lv = 0, reached_leaf = 0, do_pop = 0;
-        while (lv < 3) {
+        while (lv < g_levels) {
             const uint32_t* tn = s->tree + 4 * (size_t)node;
             uint32_t ax = tn[0] & 3u;
             if (ax == 3u) {
@@ -165,6 +167,82 @@ int walk_sim(const uint32_t* tree, const float* planes, const uint32_t* ids, con
             tv = ~0u;
             int fv = walk(&s, v, o, d, r[6], r[7], flags[i] & 1, &hv, &tv, out + v * S_N);
             if (fv != f0 || (f0 && (hv != h0 || tv != t0))) out[v * S_N + S_BAD] += 1;
+        }
+    }
+    return 0;
+}
+
+/* Compact-trail model: the trail's pending
+ * entries in push order, K slots per lane in LDS as a ring (entry p in slot
+ * p mod K, written on push only), an entry overwritten by a later push is "lost"
+ * and must be recomputed when popped (its value is the t of the entry below it,
+ * (plane - o)/d at an ancestor: a node load and an exact division).  Per ray and
+ * K in ks[0..nk): out[k*4 + 0] pushes, +1 pushes that overwrite a pending entry,
+ * +2 pops, +3 pops of lost entries.  Closest-hit walk of v0 (anyhit per flags). */
+int trail_sim(const uint32_t* tree, const float* planes, const uint32_t* ids, const float* pos, const uint32_t* idx,
+              const float* rays, const uint32_t* flags, uint32_t n, const uint32_t* ks, uint32_t nk, double* out)
+{
+    Scene s = {tree, planes, ids, pos, idx};
+    memset(out, 0, sizeof(double) * 4 * nk);
+    for (uint32_t i = 0; i < n; i++) {
+        const float* r = rays + 8 * (size_t)i;
+        v3 o = V(r[0], r[1], r[2]), d = V(r[3], r[4], r[5]);
+        float tmin = r[6], tmax = r[7];
+        int anyhit = flags[i] & 1;
+        uint32_t stk_node[64];
+        float stk_t[64], stk_tmax[64];
+        int owner[16][64];
+        for (uint32_t k = 0; k < nk; k++)
+            for (int q = 0; q < 64; q++) owner[k][q] = -1;
+        int sp = 0;
+        uint32_t node = 0;
+        for (;;) {
+            const uint32_t* tn = s.tree + 4 * (size_t)node;
+            uint32_t ax = tn[0] & 3u;
+            if (ax == 3u) {
+                uint32_t cnt = tn[0] >> 2, first = tn[1];
+                int found = 0;
+                for (uint32_t j = 0; j < cnt; j++) {
+                    float dd;
+                    if (tri(&s, s.ids[first + j], o, d, tmin, tmax, &dd)) {
+                        tmax = dd;
+                        found = 1;
+                        if (anyhit) break;
+                    }
+                }
+                if (found || sp == 0) break;
+                sp--;
+                for (uint32_t k = 0; k < nk; k++) {
+                    out[4 * k + 2] += 1;
+                    if (owner[k][sp % ks[k]] != sp) out[4 * k + 3] += 1;
+                }
+                node = stk_node[sp];
+                tmin = stk_t[sp];
+                tmax = stk_tmax[sp];
+                continue;
+            }
+            float ad = comp(d, (int)ax), ao = comp(o, (int)ax);
+            uint32_t nearn = ad >= 0.0f ? tn[2] : tn[3], farn = ad >= 0.0f ? tn[3] : tn[2];
+            float den = fabsf(ad) < 1.0e-8f ? 1.0e-8f : ad;
+            float t = (s.planes[node] - ao) / den;
+            if (t > tmax) {
+                node = nearn;
+            } else if (t < tmin) {
+                node = farn;
+            } else {
+                for (uint32_t k = 0; k < nk; k++) {
+                    out[4 * k] += 1;
+                    int q = sp % ks[k];
+                    if (owner[k][q] >= 0 && owner[k][q] < sp) out[4 * k + 1] += 1;
+                    owner[k][q] = sp;
+                }
+                stk_node[sp] = farn;
+                stk_t[sp] = t;
+                stk_tmax[sp] = tmax;
+                sp++;
+                tmax = t;
+                node = nearn;
+            }
         }
     }
     return 0;

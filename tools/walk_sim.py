@@ -71,10 +71,20 @@ def main():
     out = np.zeros(30, np.float64)
     L = lib()
     P = ctypes.c_void_p
+    L.walk_sim_levels(int(os.environ.get("WALK_LEVELS", "3")))
     L.walk_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
                P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
                P(out.ctypes.data))
     out = out.reshape(3, 10)
+    ks = np.array([4, 6, 8, 10, 12, 16], np.uint32)
+    tr = np.zeros(4 * len(ks), np.float64)
+    L.trail_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
+                P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
+                P(ks.ctypes.data), ctypes.c_uint32(len(ks)), P(tr.ctypes.data))
+    tr = tr.reshape(len(ks), 4) / len(R)
+    for k, row in zip(ks, tr):
+        print(f"compact trail K={k}: per ray {row[0]:.2f} pushes, {row[1]:.3f} overwrite a pending entry, "
+              f"{row[2]:.2f} pops, {row[3]:.3f} pops of a lost entry (recompute)")
     print(f"config {cfgn}: {len(R)} rays ({sum(flags)} any-hit), {time.time() - t0:.1f} s")
     for v in range(3):
         s = {k: round(out[v, i] / len(R), 3) for i, k in enumerate(NAMES)}
