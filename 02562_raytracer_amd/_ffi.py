@@ -31,6 +31,7 @@ RT_OPT_SHADE_THRESHOLD = 3
 RT_OPT_SAMPLE_CHUNK = 4
 RT_OPT_SAMPLE_BUDGET_MB = 5
 RT_OPT_UNIT_ORDER = 6
+RT_OPT_BSP_CULL = 9
 RT_OPT_KERNEL_TIMING = 7
 
 MODES = {"W1E6": RT_MODE_W1E6, "W6E1": RT_MODE_W6E1, "PROJECT": RT_MODE_PROJECT, "W7E3": RT_MODE_W7E3,
@@ -93,7 +94,7 @@ class Tileset(C.Structure):
 COUNT_FIELDS = ["samples", "primary", "shadow", "bounce", "node_interior", "node_leaf", "bvh_pops",
                 "ids_read", "tri_tests", "tri_accepts", "trips", "lane_steps", "leaf_lane_steps",
                 "node_trips", "leaf_trips", "exact_tests", "exact_nodes", "shade_passes",
-                "shade_lanes", "trav_cycles", "shade_cycles", "memwait_cycles"]
+                "shade_lanes", "trav_cycles", "shade_cycles", "memwait_cycles", "subtree_culls"]
 
 
 class RayCounts(C.Structure):

@@ -64,6 +64,8 @@ struct rt_ctx {
     int shade_threshold = -1;   // -1: per walk (BSP 8, BVH 4); pixel-major units refill together (coherent samples)
     uint32_t sample_chunk = 1;          // iterations per k_path work unit
     uint32_t unit_order = 1;            // 0: chunk-major, 1: pixel-major
+    uint32_t bsp_cull = 1;              // RT_OPT_BSP_CULL: subtree culling by content boxes in the BSP walk
+    float bsp_margin = 0.0f;            // its scene margin: 2^-10 x the scene's coordinate magnitude (set on upload)
     uint64_t sample_budget_mb = 16384;  // per-sample scratch (one pass at 1080p x 256 spp needs 8.1 GiB)
     DevBuf samples;
     bool detail = false;
@@ -271,6 +273,10 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
     case RT_OPT_KERNEL_TIMING:
         c->ktiming = value != 0;
         return RT_OK;
+    case RT_OPT_BSP_CULL:
+        if (value < 0 || value > 1) return fail(c, RT_E_INVALID, "BSP cull must be 0 or 1");
+        c->bsp_cull = (uint32_t)value;
+        return RT_OK;
     case RT_OPT_UNIT_ORDER:
         if (value < 0 || value > 1) return fail(c, RT_E_INVALID, "unit order must be 0 or 1");
         c->unit_order = (uint32_t)value;
@@ -414,6 +420,28 @@ int rt_upload_mesh(rt_ctx* c, const float* pos_vec4, const float* nrm_vec4, uint
     return RT_OK;
 }
 
+// The traversal layout of the context's BSP (reference arrays already in
+// bsp_ref_tree / bsp_ref_planes / bsp_ids, mesh in pos / idx): content boxes,
+// 80-B treelets and the 48-B records (rt_bsp_build.hip launch_bsp_repack), and
+// the content boxes' scene margin: 2^-10 of the largest coordinate magnitude of
+// the BSP's root box (bsp_box_miss in rt_kernels.hip adds the ray origin's).
+static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off, size_t total, const float aabb[8])
+{
+    HIPCHK(c, c->bsp_nodes.alloc(total));
+    DevBuf boxes;
+    HIPCHK(c, boxes.alloc((size_t)nnodes * 32));
+    if (rtk::launch_bsp_repack(c->bsp_ref_tree.as<uint32_t>(), c->bsp_ref_planes.as<float>(), nnodes,
+                               (uint32_t)rec_off, c->bsp_nodes.p, c->pos.as<float4>(), c->idx.as<uint4>(),
+                               c->bsp_ids.as<uint32_t>(), nids, 0.0f, boxes.p, c->stream))
+        return fail(c, RT_E_DEVICE, "BSP repack launch failed");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    float scale = 0.0f;
+    for (int k : {0, 1, 2, 4, 5, 6})
+        if (std::isfinite(aabb[k])) scale = std::max(scale, std::fabs(aabb[k]));
+    c->bsp_margin = std::ldexp(scale, -10);
+    return RT_OK;
+}
+
 int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const float* planes, uint32_t nnodes,
                   const uint32_t* ids, uint32_t nids, uint32_t max_depth)
 {
@@ -443,59 +471,30 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
         stack.push_back((uint32_t)l);
         stack.push_back((uint32_t)rgt);
     }
-    std::vector<float> recs;
-    build_recs(c->h_pos, c->h_idx, ids, nids, recs);
     if (int r = set_dev(c)) return r;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->has_bsp = false;
     int r;
     // One allocation [treelets | records], read through one buffer resource
-    // with 32-bit offsets (DESIGN.md "Data layout in HBM"):
-    //  * treelet of node M (1-based heap index), 64 B at 64*M: the 8-B nodes
-    //    {M, 2M | 2M+1, pad | 4M, 4M+1 | 4M+2, 4M+3} -- everything a 3-level walk
-    //    from M reads, in one 64-B line;
+    // with 32-bit offsets (DESIGN.md "Data layout in HBM"), laid out on the
+    // device by launch_bsp_repack from the reference arrays (the same code as
+    // rt_build_bsp_device):
+    //  * treelet of node M (1-based heap index), 80 B at 80*M: M's content box
+    //    and the 8-B nodes {M | 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3} -- everything
+    //    a 3-level walk from M reads;
     //  * 8-B node: interior {axis, plane bits}; leaf {3 | (48*count) << 2, byte
     //    offset of its first record} (children implicit: 2i+1, 2i+2 0-based);
     //  * record k (treeIds slot k): 48 B {v0, e0, e1, n} at rec_off + 48*k.
     const size_t slots = (size_t)nnodes + 1;
-    const size_t rec_off = (slots * 64 + 255) & ~(size_t)255;
-    const size_t total = rec_off + recs.size() * 4;
+    const size_t rec_off = (slots * rtk::BSP_TREELET_BYTES + 255) & ~(size_t)255;
+    const size_t total = rec_off + (size_t)nids * 48;
     if (total >= ((size_t)1 << 32))
         return fail(c, RT_E_UNSUPPORTED, "rt_upload_bsp: BSP treelets + records must stay below 4 GiB (max_depth <= 24)");
-    {
-        auto node8 = [&](size_t m, uint32_t* o) {   // 1-based m; zero beyond the tree
-            if (m == 0 || m > nnodes) {
-                o[0] = o[1] = 0u;
-                return;
-            }
-            const uint32_t* n = tree + 4 * (m - 1);
-            if ((n[0] & 3u) == 3u) {
-                o[0] = 3u | ((48u * (n[0] >> 2)) << 2);
-                o[1] = (uint32_t)(rec_off + 48ull * n[1]);
-            } else {
-                o[0] = n[0] & 3u;
-                memcpy(&o[1], &planes[m - 1], 4);
-            }
-        };
-        std::vector<uint8_t> blob(total, 0);
-        uint32_t* tl = reinterpret_cast<uint32_t*>(blob.data());
-        for (size_t m = 1; m < slots; m++) {
-            uint32_t* o = tl + 16 * m;
-            node8(m, o);
-            node8(2 * m, o + 2);
-            node8(2 * m + 1, o + 4);
-            node8(4 * m, o + 8);
-            node8(4 * m + 1, o + 10);
-            node8(4 * m + 2, o + 12);
-            node8(4 * m + 3, o + 14);
-        }
-        memcpy(blob.data() + rec_off, recs.data(), recs.size() * 4);
-        if ((r = upload(c, c->bsp_nodes, blob.data(), blob.size()))) return r;
-    }
-    c->bsp_rec_off = (uint32_t)rec_off;
-    if ((r = upload(c, c->bsp_ids, ids, (size_t)nids * 4))) return r;
     if ((r = upload(c, c->bsp_ref_tree, tree, (size_t)nnodes * 16))) return r;
     if ((r = upload(c, c->bsp_ref_planes, planes, (size_t)nnodes * 4))) return r;
+    if ((r = upload(c, c->bsp_ids, ids, (size_t)nids * 4))) return r;
+    if ((r = repack_bsp(c, nnodes, nids, rec_off, total, aabb))) return r;
+    c->bsp_rec_off = (uint32_t)rec_off;
     memcpy(c->bsp_aabb8, aabb, sizeof c->bsp_aabb8);
     c->bsp_nnodes = nnodes;
     c->bsp_nids = nids;
@@ -630,21 +629,17 @@ int rt_build_bsp_device(rt_ctx* c, uint32_t max_depth, uint32_t max_leaf, rt_bsp
     if (o.ids) ids.adopt(o.ids, std::max<size_t>(16, (size_t)o.nids * 4));
     if (r) return fail(c, r, err);
     const size_t slots = (size_t)o.nnodes + 1;
-    const size_t rec_off = (slots * 64 + 255) & ~(size_t)255;
+    const size_t rec_off = (slots * rtk::BSP_TREELET_BYTES + 255) & ~(size_t)255;
     const size_t total = rec_off + (size_t)o.nids * 48;
     if (total >= ((size_t)1 << 32))
         return fail(c, RT_E_UNSUPPORTED, "rt_build_bsp_device: BSP treelets + records must stay below 4 GiB");
-    HIPCHK(c, c->bsp_nodes.alloc(total));
-    if (rtk::launch_bsp_repack(tree.as<uint32_t>(), planes.as<float>(), o.nnodes, (uint32_t)rec_off, c->bsp_nodes.p,
-                               c->pos.as<float4>(), c->idx.as<uint4>(), ids.as<uint32_t>(), o.nids, c->stream))
-        return fail(c, RT_E_DEVICE, "rt_build_bsp_device: repack launch failed");
-    HIPCHK(c, hipStreamSynchronize(c->stream));
     c->bsp_ref_tree.adopt(tree.p, tree.n);
     tree.p = nullptr;
     c->bsp_ref_planes.adopt(planes.p, planes.n);
     planes.p = nullptr;
     c->bsp_ids.adopt(ids.p, ids.n);
     ids.p = nullptr;
+    if (int rr = repack_bsp(c, o.nnodes, o.nids, rec_off, total, o.aabb)) return rr;
     c->bsp_rec_off = (uint32_t)rec_off;
     c->bsp_depth = max_depth;
     memcpy(c->bsp_aabb8, o.aabb, sizeof c->bsp_aabb8);
@@ -800,6 +795,8 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bvh_rec_off = c->bvh_rec_off;
     S.bvh_ids = c->bvh_ids.as<uint32_t>();
     S.bvh_nnodes = c->bvh_nnodes;
+    S.bsp_cull = c->bsp_cull;
+    S.bsp_margin = c->bsp_margin;
     return S;
 }
 

@@ -440,8 +440,56 @@ namespace rtk {
 
 // rt_upload_bsp's repack on device: the 64-B treelet of every 1-based node M
 // (nodes M, 2M, 2M+1, 4M..4M+3 as 8-B entries) and the 48-B triangle records.
+// Content box of every node's subtree: the union of the bounding boxes of the
+// triangles its leaves reference (2 x float4 per node: min, max; empty: +inf /
+// -inf).  The BSP walk skips a subtree whose box the ray interval misses
+// (rt_kernels.hip bsp_walk, DESIGN.md section 4 "Subtree culling").
+// Leaves first (a leaf range outside ids -- an unreachable node -- stays empty),
+// then the interior nodes one depth at a time, bottom-up.
+__global__ void __launch_bounds__(256) k_leaf_boxes(const uint32_t* tree, uint32_t nnodes, const float4* pos,
+                                                    const uint4* idx, const uint32_t* ids, uint32_t nids, float4* box)
+{
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nnodes; i += gridDim.x * 256u) {
+        const uint32_t n0 = tree[4 * (size_t)i], first = tree[4 * (size_t)i + 1];
+        float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+        const uint32_t cnt = (n0 & 3u) == 3u ? n0 >> 2 : 0u;
+        if ((uint64_t)first + cnt <= nids) {
+            for (uint32_t k = 0; k < cnt; k++) {
+                const uint4 ix = idx[ids[first + k]];
+                const float4 v[3] = {pos[ix.x], pos[ix.y], pos[ix.z]};
+                for (int j = 0; j < 3; j++) {
+                    lo.x = fminf(lo.x, v[j].x);
+                    lo.y = fminf(lo.y, v[j].y);
+                    lo.z = fminf(lo.z, v[j].z);
+                    hi.x = fmaxf(hi.x, v[j].x);
+                    hi.y = fmaxf(hi.y, v[j].y);
+                    hi.z = fmaxf(hi.z, v[j].z);
+                }
+            }
+        }
+        box[2 * (size_t)i] = lo;
+        box[2 * (size_t)i + 1] = hi;
+    }
+}
+__global__ void __launch_bounds__(256) k_node_boxes(const uint32_t* tree, uint32_t nnodes, uint32_t lo_i, uint32_t hi_i,
+                                                    float4* box)
+{
+    for (uint32_t i = lo_i + blockIdx.x * 256u + threadIdx.x; i < hi_i; i += gridDim.x * 256u) {
+        if ((tree[4 * (size_t)i] & 3u) == 3u || 2ull * i + 2 >= nnodes) continue;   // a leaf (done) / no children
+        const float4 a0 = box[2 * (2 * (size_t)i + 1)], a1 = box[2 * (2 * (size_t)i + 1) + 1];
+        const float4 b0 = box[2 * (2 * (size_t)i + 2)], b1 = box[2 * (2 * (size_t)i + 2) + 1];
+        box[2 * (size_t)i] = make_float4(fminf(a0.x, b0.x), fminf(a0.y, b0.y), fminf(a0.z, b0.z), 0.0f);
+        box[2 * (size_t)i + 1] = make_float4(fmaxf(a1.x, b1.x), fmaxf(a1.y, b1.y), fmaxf(a1.z, b1.z), 0.0f);
+    }
+}
+
+// The 80-B treelet of 1-based node M at 80*M (rt_internal.h BSP_TREELET_BYTES):
+// {box min.xyz, max.x | max.y, max.z, node M | nodes 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3}
+// -- node M's content box, expanded by `margin` on every side, and the 8-B
+// nodes a three-level walk from M reads (interior {axis, plane bits}; leaf
+// {3 | (48*count) << 2, byte offset of its first record}).
 __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes,
-                                                    uint32_t rec_off, uint2* tl)
+                                                    uint32_t rec_off, const float4* box, float margin, uint32_t* tl)
 {
     const size_t slots = (size_t)nnodes + 1;
     for (size_t m = (size_t)blockIdx.x * 256u + threadIdx.x; m < slots; m += (size_t)gridDim.x * 256u) {
@@ -451,19 +499,20 @@ __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const 
             if ((n[0] & 3u) == 3u) return make_uint2(3u | ((48u * (n[0] >> 2)) << 2), rec_off + 48u * n[1]);
             return make_uint2(n[0] & 3u, __float_as_uint(planes[q - 1]));
         };
-        uint2* o = tl + 8 * m;
+        uint32_t* o = tl + 20 * m;
         if (m == 0) {
-            for (int k = 0; k < 8; k++) o[k] = make_uint2(0u, 0u);
+            for (int k = 0; k < 20; k++) o[k] = 0u;
             continue;
         }
-        o[0] = node8(m);
-        o[1] = node8(2 * m);
-        o[2] = node8(2 * m + 1);
-        o[3] = make_uint2(0u, 0u);
-        o[4] = node8(4 * m);
-        o[5] = node8(4 * m + 1);
-        o[6] = node8(4 * m + 2);
-        o[7] = node8(4 * m + 3);
+        const float4 lo = box[2 * (m - 1)], hi = box[2 * (m - 1) + 1];
+        const float b[6] = {lo.x - margin, lo.y - margin, lo.z - margin, hi.x + margin, hi.y + margin, hi.z + margin};
+        for (int k = 0; k < 6; k++) o[k] = __float_as_uint(b[k]);
+        const uint2 n[7] = {node8(m), node8(2 * m), node8(2 * m + 1), node8(4 * m), node8(4 * m + 1), node8(4 * m + 2),
+                            node8(4 * m + 3)};
+        for (int k = 0; k < 7; k++) {
+            o[6 + 2 * k] = n[k].x;
+            o[7 + 2 * k] = n[k].y;
+        }
     }
 }
 
@@ -483,11 +532,23 @@ __global__ void __launch_bounds__(256) k_tri_records2(const float4* pos, const u
 }
 
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
-                      const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, hipStream_t s)
+                      const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,
+                      void* box_scratch, hipStream_t s)
 {
+    // content boxes: leaves, then each depth bottom-up (depth d holds nodes [2^d - 1, 2^(d+1) - 1))
+    float4* box = reinterpret_cast<float4*>(box_scratch);
+    const uint32_t g0 = std::min<uint32_t>(16384, (nnodes + 255) / 256);
+    hipLaunchKernelGGL(k_leaf_boxes, dim3(g0), dim3(256), 0, s, tree, nnodes, pos, idx, ids, nids, box);
+    uint32_t depth = 0;
+    while ((2ull << depth) - 1 < nnodes) depth++;   // the deepest level
+    for (int d = (int)depth - 1; d >= 0; d--) {
+        const uint32_t lo = (1u << d) - 1u, hi = std::min<uint32_t>(nnodes, (2u << d) - 1u);
+        const uint32_t g = std::min<uint32_t>(16384, (hi - lo + 255) / 256);
+        hipLaunchKernelGGL(k_node_boxes, dim3(g), dim3(256), 0, s, tree, nnodes, lo, hi, box);
+    }
     const uint32_t g1 = std::min<uint32_t>(16384, (nnodes + 256) / 256 + 1);
-    hipLaunchKernelGGL(k_bsp_repack, dim3(g1), dim3(256), 0, s, tree, planes, nnodes, rec_off,
-                       reinterpret_cast<uint2*>(blob));
+    hipLaunchKernelGGL(k_bsp_repack, dim3(g1), dim3(256), 0, s, tree, planes, nnodes, rec_off, box, margin,
+                       reinterpret_cast<uint32_t*>(blob));
     if (nids) {
         const uint32_t g2 = std::min<uint32_t>(16384, (nids + 255) / 256 + 1);
         hipLaunchKernelGGL(k_tri_records2, dim3(g2), dim3(256), 0, s, pos, idx, ids, nids,

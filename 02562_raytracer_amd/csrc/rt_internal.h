@@ -19,10 +19,11 @@ struct DevScene {
     const rt_material* mats;
     const uint32_t* lights;
     uint32_t nverts, ntris, nmats, nlights;
-    // BSP: one allocation [64-B treelets | 48-B records] (rt_api.cpp rt_upload_bsp):
-    // treelet of 1-based node M at 64*M holds nodes M, 2M, 2M+1, 4M..4M+3 (8 B each:
-    // interior {axis, plane bits}, leaf {3 | (48*count) << 2, first record's byte offset});
-    // children implicit (2i+1, 2i+2 0-based, src/data_structures/bsp_tree.rs:137-140).
+    // BSP: one allocation [80-B treelets | 48-B records] (rt_api.cpp rt_upload_bsp):
+    // treelet of 1-based node M at 80*M holds M's content box (min.xyz, max.xyz: the
+    // triangles its subtree references, expanded) and nodes M, 2M, 2M+1, 4M..4M+3 (8 B
+    // each: interior {axis, plane bits}, leaf {3 | (48*count) << 2, first record's byte
+    // offset}); children implicit (2i+1, 2i+2 0-based, src/data_structures/bsp_tree.rs:137-140).
     const uint2* bsp_nodes;       // start of the allocation
     const float4* bsp_recs;       // = bsp_nodes + bsp_rec_off: v0, e0=v1-v0, e1=v2-v0, n=cross(e0,e1)
     uint32_t bsp_bytes;           // size of the allocation (buffer-resource range)
@@ -37,6 +38,8 @@ struct DevScene {
     uint32_t bvh_rec_off;
     const uint32_t* bvh_ids;
     uint32_t bvh_nnodes;
+    uint32_t bsp_cull;            // the BSP walk skips subtrees whose content box the ray misses (RT_OPT_BSP_CULL)
+    float bsp_margin;             // the content boxes' scene margin (rt_kernels.hip bsp_box_miss)
 };
 
 // Work mapping + outputs of one launch.
@@ -115,9 +118,13 @@ struct BspDeviceOut {
 };
 int build_bsp_device(const float4* pos, const uint4* idx, uint32_t ntris, uint32_t max_depth, uint32_t max_leaf,
                      int num_cus, hipStream_t stream, BspDeviceOut& out, rt_bsp_build_times* times, std::string& err);
-// traversal layout of a BSP from its reference-layout arrays (rt_upload_bsp's repack, on device)
+// traversal layout of a BSP from its reference-layout arrays (rt_upload_bsp's repack, on device):
+// 80-B treelets (content box + 7 nodes, BSP_TREELET_BYTES) then the 48-B records;
+// box_scratch: nnodes x 32 B of device memory for the content boxes
+constexpr uint32_t BSP_TREELET_BYTES = 80;
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
-                      const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, hipStream_t stream);
+                      const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,
+                      void* box_scratch, hipStream_t stream);
 // device primitives shared by the builders (rt_build.hip)
 int scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* scratch, hipStream_t s);
 size_t scan_scratch_words(uint32_t n);

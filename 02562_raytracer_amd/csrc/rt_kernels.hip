@@ -101,7 +101,7 @@ __device__ __forceinline__ float rnd(uint32_t& prev) { return (float)mcg31(prev)
 // ------------------------------------------------------------------ counters
 enum { C_SAMPLES, C_PRIMARY, C_SHADOW, C_BOUNCE, C_INTERIOR, C_LEAF, C_POPS, C_IDS, C_TESTS, C_ACCEPTS,
        C_TRIPS, C_LANE_STEPS, C_LEAF_LANE_STEPS, C_NODE_TRIPS, C_LEAF_TRIPS, C_EXACT_TESTS, C_EXACT_NODES,
-       C_SHADE_PASSES, C_SHADE_LANES, C_TRAV_CYC64, C_SHADE_CYC64, C_MEMWAIT_CYC64, C_N };
+       C_SHADE_PASSES, C_SHADE_LANES, C_TRAV_CYC64, C_SHADE_CYC64, C_MEMWAIT_CYC64, C_CULLS, C_N };
 
 struct Counters {
     uint32_t v[C_N];
@@ -520,11 +520,11 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 #define RT_LEAF_TESTS 2   // triangle tests per leaf trip of the BSP walk: 1 or 2
 #endif
 template <bool COUNT, bool CULL, class LOG>
-__device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const f3 o, const f3 d,
-                                               bool anyhit, Trav& t, Counters& c, LOG& lg)
+__device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const v4u r1, const f3 o,
+                                               const f3 d, bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
     if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
-        const v4u r1 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 16u, 0, 0);
+        // the trip's 80-B load holds this record's first 32 B (nx, r1)
         const v4u r2 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
         lg.tested(t.leaf_k);
         if (COUNT) {
@@ -553,8 +553,8 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
 // RT_LEAF_TESTS 2, the next one, whose first 16 B are q3).
 template <bool COUNT, bool CULL, class LOG>
 __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, const v4u q0, const v4u q1, const v4u q2,
-                                               const v4u q3, const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c,
-                                               bool& done, bool& pop, LOG& lg)
+                                               const v4u q3, const v4u q4, const f3 o, const f3 d, bool anyhit, Trav& t,
+                                               Counters& c, bool& done, bool& pop, LOG& lg)
 {
     lg.tested(t.leaf_k);
     if (COUNT) {
@@ -574,35 +574,75 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
         }
     }
     t.leaf_k += 48u;
-    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, o, d, anyhit, t, c, lg);
+    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, q4, o, d, anyhit, t, c, lg);
     const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
     done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
     pop = leaf_done & !t.found;
 }
 
+// Subtree culling (RT_OPT_BSP_CULL, DESIGN.md section 4 "Subtree culling"): a
+// trip that starts at node M first tests the ray interval [tmin, tmax] against
+// M's content box -- the union of the bounding boxes of the triangles M's
+// leaves reference -- grown by a margin of 2^-10 of the larger of the scene's
+// and the ray origin's coordinate magnitude (dscene = 2^-10 x the scene's).  If
+// the interval misses it by a clear gap, no triangle of the subtree can be
+// accepted inside the interval, so the reference's walk of that subtree
+// (bsp.wgsl:10-81: every leaf tested without a hit, every pending entry pushed
+// inside it popped again) ends where the next pop starts: the walk pops at
+// once.  Which triangle is hit, and where, does not change; only hitless work
+// is skipped.  An axis whose direction component is below the shader's 1e-8
+// cut (inv is then +-1e8 or the NaN flag, see bsp_inv1) constrains nothing: the
+// NaN drops out of fminf / fmaxf.
+__device__ __forceinline__ bool bsp_box_miss(const v4u q0, const v4u q1, const f3 o, const f3 inv, float tmin, float tmax,
+                                             float dscene)
+{
+    const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
+    const float m = __builtin_fmaxf(mo * 0x1p-10f, dscene);
+    const float bmin[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
+    const float bmax[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
+    const float oo[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
+    float tn = tmin, tf = tmax;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : __builtin_nanf("");
+        const float t1 = (bmin[a] - m - oo[a]) * ib, t2 = (bmax[a] + m - oo[a]) * ib;
+        tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
+        tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
+    }
+    // a clear gap: the rounding of the slab products cannot close it
+    return tn - tf > (rt_absf(tn) + rt_absf(tf)) * 0x1p-18f;
+}
+
 // The walking half of a BSP trip: node m (level 0), a child (level 1), a
-// grandchild (level 2) from the treelet in q0..q3.  Returns true when the walk
-// reached a non-empty leaf (its range is set, its tests start next trip); an
-// empty leaf sets pop.  (Testing the first record of a leaf in the trip that
-// reaches it -- one more round trip -- was slower: config 4 -3.7 %, config 5
-// -11 %, profiles/r02/ab_et1.txt.)
+// grandchild (level 2) from the 80-B treelet in q0..q4 (rt_internal.h:
+// {box | box, node M | 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3}).  Returns true when
+// the walk reached a non-empty leaf (its range is set, its tests start next
+// trip); an empty leaf, or a subtree culled by its content box, sets pop.
+// (Testing the first record of a leaf in the trip that reaches it -- one more
+// round trip -- was slower: config 4 -3.7 %, config 5 -11 %, profiles/r02/ab_et1.txt.)
 template <bool COUNT>
-__device__ __forceinline__ bool bsp_walk(float* stk, const v4u q0, const v4u q1, const v4u q2, const v4u q3, const f3 o,
-                                         const f3 d, const f3 inv, Trav& t, Counters& c, bool& pop)
+__device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4u q0, const v4u q1, const v4u q2,
+                                         const v4u q3, const v4u q4, const f3 o, const f3 d, const f3 inv, Trav& t,
+                                         Counters& c, bool& pop)
 {
     uint32_t m = t.node;
+    if (S.bsp_cull && bsp_box_miss(q0, q1, o, inv, t.tmin, t.tmax, S.bsp_margin)) {
+        if (COUNT) c.v[C_CULLS]++;
+        pop = true;
+        return false;
+    }
     const uint32_t dep = heap_depth(m);
-    uint2 n = make_uint2(q0.x, q0.y);
+    uint2 n = make_uint2(q1.z, q1.w);
     bool leaf = (n.x & 3u) == 3u;
     if (!leaf) {
         // the trail slot of this level (RT_TRAIL_SLOT), or the trail base
         float* const s0 = RT_TRAIL_SLOT ? stk + dep * 256u : stk;
         m = bsp_decide<COUNT>(s0, n, m, dep, o, d, inv, t, c);
-        n = (m & 1u) ? make_uint2(q1.x, q1.y) : make_uint2(q0.z, q0.w);
+        n = (m & 1u) ? make_uint2(q2.z, q2.w) : make_uint2(q2.x, q2.y);
         leaf = (n.x & 3u) == 3u;
         if (!leaf) {
             m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 256 : stk, n, m, dep + 1u, o, d, inv, t, c);
-            const v4u g = (m & 2u) ? q3 : q2;
+            const v4u g = (m & 2u) ? q4 : q3;
             n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
             leaf = (n.x & 3u) == 3u;
             if (!leaf) m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 512 : stk, n, m, dep + 2u, o, d, inv, t, c);
@@ -625,23 +665,26 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
     const bool in_leaf = t.leaf_k != t.leaf_end;
-    const uint32_t base = in_leaf ? t.leaf_k : t.node << 6;
+    // a leaf lane: its next 80 B of records (one whole, the next one's first
+    // 32 B); a walking lane: the 80-B treelet of its node
+    const uint32_t base = in_leaf ? t.leaf_k : t.node * BSP_TREELET_BYTES;
     uint64_t tw = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
     v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
     v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
     v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 48u, 0, 0);
-    // keep the four loads together (the compiler would sink q2/q3 into the
-    // level-2 branch: a second round trip)
-    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
+    v4u q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 64u, 0, 0);
+    // keep the five loads together (the compiler would sink the later ones
+    // into the level-2 branch: a second round trip)
+    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4));
     if (COUNT) {   // diagnostics: cycles from issuing the loads to their data
         tw = __builtin_amdgcn_s_memtime() - tw;
         if ((threadIdx.x & 63u) == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u))
             c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
     }
     bool done = false, pop = false;
-    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, o, d, anyhit, t, c, done, pop, lg);
-    else bsp_walk<COUNT>(stk, q0, q1, q2, q3, o, d, inv, t, c, pop);
+    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, o, d, anyhit, t, c, done, pop, lg);
+    else bsp_walk<COUNT>(S, stk, q0, q1, q2, q3, q4, o, d, inv, t, c, pop);
     if (pop) done = bsp_pop(stk, t);
     return done;
 }

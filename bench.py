@@ -179,8 +179,11 @@ def main():
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)
+    ap.add_argument("--bsp-cull", type=int, default=None, help="RT_OPT_BSP_CULL (default 1: subtree culling on)")
     ap.add_argument("--dump-frame", default=None,
                     help="rank 0 saves the last step's assembled frame (accum + ids) to this .npz")
+    ap.add_argument("--progress", action="store_true",
+                    help="a stderr line after every timed step (a host synchronisation per step)")
     ap.add_argument("--rank-share", type=int, default=None,
                     help="profiling: one process renders only rank 0's share of an N-rank split (the work one GPU "
                          "of the N-GPU bench does); its roofline is looked up under the _nN PMC key")
@@ -228,7 +231,7 @@ def main():
     trav = args.trav or wl.traversal
     cam = wl.camera
 
-    t0 = time.perf_counter()
+    t0 = t_start = time.perf_counter()
     mesh = wl.mesh(args.ntris)
     ctx = rt.Context(local)
     ctx.set_stream(stream.cuda_stream)
@@ -240,6 +243,8 @@ def main():
         ctx.set_option(rt._ffi.RT_OPT_SAMPLE_CHUNK, args.sample_chunk)
     if args.unit_order is not None:
         ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, args.unit_order)
+    if args.bsp_cull is not None:
+        ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, args.bsp_cull)
     ctx.upload_mesh(mesh)
     if trav == "BSP":
         accel = mesh.bsp_tree()
@@ -278,16 +283,24 @@ def main():
             ctx.unpack_tiles(W, H, 1, acc_local.data_ptr(), ids_local.data_ptr(), frame.data_ptr(),
                              frame_ids.data_ptr())
 
+    def progress(msg):   # stderr heartbeat: a long configuration (config 5 at 1024 spp) is not silent for minutes
+        print(f"[bench rank {rank}] {msg} ({time.perf_counter() - t_start:.1f} s)", file=sys.stderr, flush=True)
+
+    progress(f"setup done in {setup_s:.1f} s")
     # counted step (also the first warm-up): rays per step, deterministic
     step()
     counts = ctx.last_counts()
+    progress("counted step done")
     # counting instantiation: traversal counters for the algorithmic bytes
     ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 1)
     step()
     detail = ctx.last_counts()
     ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
+    progress("counting-instantiation step done")
     for _ in range(max(0, args.warmup - 1)):
         step()
+        torch.cuda.synchronize(dev)
+        progress("warm-up step done")
 
     rays = torch.tensor([counts["primary"] + counts["shadow"], counts["primary"], counts["shadow"],
                          counts["bounce"], algorithmic_bytes(detail, trav)],
@@ -307,6 +320,9 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
+        if args.progress:   # (a host sync per step: off unless asked, the steps stay back to back)
+            torch.cuda.synchronize(dev)
+            progress(f"timed step {k + 1}/{args.steps} done")
     torch.cuda.synchronize(dev)
     if use_dist:
         dist.barrier()
@@ -356,7 +372,7 @@ def main():
                                                             "leaf_lane_steps", "node_trips", "leaf_trips",
                                                             "exact_tests", "exact_nodes", "shade_passes",
                                                             "shade_lanes", "trav_cycles", "shade_cycles",
-                                                            "memwait_cycles")},
+                                                            "memwait_cycles", "subtree_culls")},
             "simd_lane_util": round(detail["lane_steps"] / max(1, 64 * detail["trips"]), 4),
             "setup_s": round(setup_s, 3),
         }

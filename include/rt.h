@@ -155,6 +155,7 @@ typedef struct rt_ray_counts {
     uint64_t trav_cycles;
     uint64_t shade_cycles;
     uint64_t memwait_cycles; /* BSP trips: wave cycles from load issue to data */
+    uint64_t subtree_culls;  /* BSP walking trips that skipped their node's subtree (content box missed) */
 } rt_ray_counts;
 
 /* ---- options (rt_set_option) ------------------------------------------- */
@@ -168,6 +169,10 @@ typedef struct rt_ray_counts {
 /* option 8 is retired (trip-half postponement: slower on every BASELINE workload, and its
    per-trip test cost 1.7-4.4 % even when off, profiles/r02/sweep_KH_c5.txt, ab_nokh.txt) */
 #define RT_OPT_UNIT_ORDER      6  /* W7E3/W9E1 work-unit order: 0 chunk-major, 1 pixel-major (default) */
+#define RT_OPT_BSP_CULL        9  /* 1 (default): the BSP walk skips a subtree whose content box (the union of its
+                                     triangles' bounding boxes, grown by a margin) the ray interval misses -- the hit
+                                     is the same, the hitless work is skipped; 0: every node of bsp.wgsl's walk is
+                                     visited (the reference's tested-triangle sequence) */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
 

@@ -16,7 +16,8 @@ class Scene:
     uploads its own (rt.Mesh -> BspTree/Bvh -> Context), the oracle builds its
     own from the same triangle arrays."""
 
-    def __init__(self, rt, mesh, trav, env=(1.0, 1.0, 1.0), oracle_mesh=None, device=0, oracle_accel_from_product=False):
+    def __init__(self, rt, mesh, trav, env=(1.0, 1.0, 1.0), oracle_mesh=None, device=0, oracle_accel_from_product=False,
+                 bsp_depth=20, bsp_leaf=4):
         """oracle_accel_from_product: the oracle renders from the product
         builder's arrays instead of building its own (they are bit-identical,
         tests/test_host_builders.py) -- for the 7M/10M-triangle configs, where
@@ -29,9 +30,10 @@ class Scene:
         ctx.upload_mesh(mesh)
         self.obsp = self.obvh = None
         if trav == "BSP":
-            bsp = mesh.bsp_tree()
+            bsp = mesh.bsp_tree(bsp_depth, bsp_leaf)
             ctx.upload_bsp(bsp)
-            self.obsp = O.OracleBsp(*bsp.arrays()) if oracle_accel_from_product else O.build_bsp(self.om)
+            self.obsp = (O.OracleBsp(*bsp.arrays()) if oracle_accel_from_product
+                         else O.build_bsp(self.om, bsp_depth, bsp_leaf))
         elif trav == "BVH":
             bvh = mesh.bvh()
             ctx.upload_bvh(bvh)

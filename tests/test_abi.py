@@ -40,7 +40,7 @@ def test_struct_sizes(rt):
     assert C.sizeof(F.Material) == 64        # src/mesh.rs:12-20
     assert C.sizeof(F.GpuNode) == 32         # hlbvh.rs:508-528
     assert C.sizeof(F.Uniform) == 80         # uniform.rs:6-34
-    assert C.sizeof(F.RayCounts) == 22 * 8
+    assert C.sizeof(F.RayCounts) == 23 * 8
 
 
 def test_error_codes_without_gpu(rt):

@@ -31,6 +31,9 @@ def _bits(x):
 def _scene(rt, oracle, name, trav):
     m = oracle.load_obj(model(f"{name}.obj"))
     ctx = rt.Context(0)
+    # the reference's own walk, node by node: no subtree culling (the tested-triangle
+    # sequence is compared); test_secondary_rays_culled_walk_same_hits turns it on
+    ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, 0)
     ctx.upload_mesh_arrays(m.pos, m.nrm, m.idx, m.mats, m.lights)
     if trav == "BSP":
         acc = oracle.build_bsp(m, 20, 4, js64=True)
@@ -112,10 +115,32 @@ def test_secondary_rays_bvh_walk_matches_oracle(rt, oracle, name):
             assert h["tri"][i] == q["tested"][k - 1]   # it stopped at its first accept
 
 
+@pytest.mark.parametrize("name", SCENES)
+def test_secondary_rays_culled_walk_same_hits(rt, oracle, name):
+    # with subtree culling (RT_OPT_BSP_CULL 1, the default) the walk skips subtrees
+    # whose content box the ray interval misses: fewer triangles are tested (a
+    # subsequence of the reference's), and every ray's hit -- triangle, distance,
+    # barycentrics, the any-hit boolean -- is the same bit for bit
+    meta, z = load_fixture(name)
+    ctx, sc = _scene(rt, oracle, name, "BSP")
+    try:
+        shadow = z["kind"] == 1
+        h0 = ctx.trace_rays("BSP", _rays(z), anyhit=shadow)
+        ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, 1)
+        h1 = ctx.trace_rays("BSP", _rays(z), anyhit=shadow)
+    finally:
+        ctx.close()
+    for k in ("tri", "dist", "beta", "gamma"):
+        assert np.array_equal(h0[k].view(np.uint32), h1[k].view(np.uint32)), k
+    assert np.all(h1["ntested"] <= h0["ntested"])
+    assert h1["ntested"].sum() < h0["ntested"].sum()
+
+
 def test_trace_rays_edge_cases(rt, oracle):
     # no rays; a zero-length interval; a ray that starts past its tmax
     m = oracle.load_obj(model("CornellBox.obj"))
     ctx = rt.Context(0)
+    ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, 0)   # the tested sequences are compared
     try:
         ctx.upload_mesh_arrays(m.pos, m.nrm, m.idx, m.mats, m.lights)
         b = oracle.build_bsp(m, 20, 4)

@@ -160,6 +160,31 @@ def test_bunny_w9e1_bvh_region(rt, gpu):
     check(g, o)
 
 
+@pytest.mark.parametrize("depth", [20, 9])
+def test_shade_threshold_is_scheduling_only(rt, gpu, depth):
+    # The shading threshold only schedules: every setting -- fixed 8 or 32,
+    # lockstep (0 and 64), and the default per-wave choice between 8 and 32 from
+    # the wave's share of lanes inside a leaf (k_path) -- renders the same bits.
+    # Depth 9 makes a test-dominated walk (~300 triangles per leaf: the share is
+    # high and the waves choose 32), depth 20 a walk-dominated one (8).
+    s = Scene(rt, rt.Mesh.synth_soup(150_000), "BSP", oracle_accel_from_product=True, bsp_depth=depth)
+    cam = ((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 1.5)
+    region = (600, 300, 96, 64)
+    frames = {}
+    try:
+        for t in (-1, 8, 32, 0, 64):
+            s.ctx.set_option(rt._ffi.RT_OPT_SHADE_THRESHOLD, t)
+            frames[t] = s.render_gpu("W9E1", cam, 1280, 720, region, 0, 3)
+    finally:
+        s.ctx.set_option(rt._ffi.RT_OPT_SHADE_THRESHOLD, -1)
+    o = s.render_oracle("W9E1", cam, 1280, 720, region, 0, 3)
+    check(frames[-1], o)
+    for t, g in frames.items():
+        assert np.array_equal(g[0].view(np.uint32), frames[-1][0].view(np.uint32)), t
+        assert np.array_equal(g[1], frames[-1][1]), t
+    s.ctx.close()
+
+
 @pytest.mark.parametrize("waves,chunk,order", [(1, 1, 1), (3, 3, 0), (32, 1, 0), (32, 5, 1)])
 def test_bvh_work_shards(rt, gpu, waves, chunk, order):
     # the BVH walk's 8 per-XCD work queues: a wave draws from its XCD's shard,
@@ -218,13 +243,17 @@ def test_detail_counters_match_oracle(rt, cornell_bsp):
     # the algorithmic-bytes inputs: traversal counters of the counting
     # instantiation equal the oracle's for primary rays (W6E1-style closest hit
     # only; shadow rays use any-hit on the GPU, a strict subset of the work)
+    # (with subtree culling off: the reference's node-by-node walk, whose counts
+    # the oracle restates; tests/test_gpu_cull.py compares culled and full walks)
     s = cornell_bsp
     gpu = s.ctx
     gpu.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 1)
+    gpu.set_option(rt._ffi.RT_OPT_BSP_CULL, 0)
     try:
         g = s.render_gpu("PROJECT", CORNELL_CAM, 64, 64, (0, 0, 64, 64))
     finally:
         gpu.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
+        gpu.set_option(rt._ffi.RT_OPT_BSP_CULL, 1)
     o = s.render_oracle("PROJECT", CORNELL_CAM, 64, 64, (0, 0, 64, 64))
     check(g, o)
     for k in ("node_interior", "node_leaf", "ids_read", "tri_tests", "tri_accepts"):

@@ -52,6 +52,31 @@ static int tri(const Scene* s, uint32_t v, v3 o, v3 w, float tmin, float tmax, f
 }
 
 int g_levels = 3;
+static uint32_t depth_of(uint32_t n0);
+static const float* g_boxes = 0;
+int g_root_only = 0;
+double g_bad[256];
+int g_bad_n = 0;
+int walk_sim_bad(double* out) { for (int i = 0; i < 4 * g_bad_n; i++) out[i] = g_bad[i]; return g_bad_n; }
+double g_cull[32], g_cull_leaf;
+void walk_sim_culls(double* out) { for (int i = 0; i < 32; i++) out[i] = g_cull[i]; out[32] = g_cull_leaf; }
+void walk_sim_root_only(int r) { g_root_only = r; }   /* nnodes x 6: content box (min.xyz, max.xyz) of each node's subtree, or NULL */
+void walk_sim_boxes(const float* b) { g_boxes = b; }
+static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
+{
+    const float* b = g_boxes + 6 * (size_t)node;
+    if (b[0] > b[3]) return 1;   /* empty subtree */
+    float t0 = tmin, t1 = tmax;
+    for (int k = 0; k < 3; k++) {
+        float dk = comp(d, k), ok = comp(o, k);
+        if (dk == 0.0f) { if (ok < b[k] || ok > b[3 + k]) return 1; continue; }
+        float a = (b[k] - ok) / dk, c = (b[3 + k] - ok) / dk;
+        if (a > c) { float x = a; a = c; c = x; }
+        if (a > t0) t0 = a;
+        if (c < t1) t1 = c;
+    }
+    return t0 > t1;
+}
 void walk_sim_levels(int l) { g_levels = l; }
 static int is_empty_leaf(const Scene* s, uint32_t node) { return (s->tree[4 * node] & 3u) == 3u && (s->tree[4 * node] >> 2) == 0; }
 static uint32_t depth_of(uint32_t n0) { uint32_t m = n0 + 1, d = 0; while (m > 1) { m >>= 1; d++; } return d; }
@@ -72,6 +97,12 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
         /* one walking trip from `node`: up to three levels */
         st[S_WT] += 1;
         int lv = 0, reached_leaf = 0, do_pop = 0;
+        if (var >= 3 && g_boxes && (node == 0 || !g_root_only) && box_miss(node, o, d, tmin, tmax)) {
+            do_pop = 1;   /* v3: the subtree's content misses the ray interval */
+            g_cull[depth_of(node) < 32 ? depth_of(node) : 31] += 1;
+            g_cull_leaf += (s->tree[4 * node] & 3u) == 3u;
+            lv = g_levels;
+        }
         while (lv < g_levels) {
             const uint32_t* tn = s->tree + 4 * (size_t)node;
             uint32_t ax = tn[0] & 3u;
@@ -113,7 +144,7 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
                 node = nearn;
             } else if (t < tmin) {
                 node = farn;
-            } else if (var >= 1 && is_empty_leaf(s, nearn)) {
+            } else if ((var == 1 || var == 2 || var == 3) && is_empty_leaf(s, nearn)) {
                 /* push + visit the empty near leaf + pop, folded: the counted
                  * leaf visit and pop of v0 are skipped */
                 tmin = t;
@@ -122,7 +153,7 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
                 st[S_PUSH] += 1;
                 stk_node[sp] = farn;
                 stk_dep[sp] = depth_of(node);
-                stk_skip[sp] = var >= 2 && is_empty_leaf(s, farn);
+                stk_skip[sp] = (var == 2 || var == 3) && is_empty_leaf(s, farn);
                 stk_t[sp] = t;
                 stk_tmax[sp] = tmax;
                 sp++;
@@ -155,18 +186,27 @@ int walk_sim(const uint32_t* tree, const float* planes, const uint32_t* ids, con
              const float* rays, const uint32_t* flags, uint32_t n, double* out)
 {
     Scene s = {tree, planes, ids, pos, idx};
-    memset(out, 0, sizeof(double) * 3 * S_N);
+    memset(out, 0, sizeof(double) * 5 * S_N);
     for (uint32_t i = 0; i < n; i++) {
         const float* r = rays + 8 * (size_t)i;
         v3 o = V(r[0], r[1], r[2]), d = V(r[3], r[4], r[5]);
         float h0 = -1, hv;
         uint32_t t0 = ~0u, tv;
         int f0 = walk(&s, 0, o, d, r[6], r[7], flags[i] & 1, &h0, &t0, out);
-        for (int v = 1; v < 3; v++) {
+        for (int v = 1; v < (g_boxes ? 5 : 3); v++) {
             hv = -1;
             tv = ~0u;
             int fv = walk(&s, v, o, d, r[6], r[7], flags[i] & 1, &hv, &tv, out + v * S_N);
-            if (fv != f0 || (f0 && (hv != h0 || tv != t0))) out[v * S_N + S_BAD] += 1;
+            if (fv != f0 || (f0 && (hv != h0 || tv != t0))) {
+                out[v * S_N + S_BAD] += 1;
+                if (g_bad_n < 64) {
+                    g_bad[g_bad_n * 4] = (double)i;
+                    g_bad[g_bad_n * 4 + 1] = (double)v;
+                    g_bad[g_bad_n * 4 + 2] = f0 ? (double)t0 : -1.0;
+                    g_bad[g_bad_n * 4 + 3] = fv ? (double)tv : -1.0;
+                    g_bad_n++;
+                }
+            }
         }
     }
     return 0;

@@ -66,16 +66,66 @@ def main():
             w = (n * np.sqrt(1 - c * c) + a * c).astype(np.float32)
             rays.append([*p, *w, 1e-4, 5000.0])
             flags.append(0)
+    if os.environ.get("WALK_STRESS"):
+        # grazing secondary rays: origin on a random triangle, direction nearly in
+        # its plane (elevation 1e-7 .. 1e-2 rad), tmin = 1e-4 (the W9E1 ETA)
+        rays, flags = [], []
+        P3 = pos[:, :3].astype(np.float64)
+        for _ in range(nr):
+            tri = int(rng.integers(idx.shape[0]))
+            v0, v1, v2 = (P3[idx[tri, k]] for k in range(3))
+            u, v = rng.random(), rng.random()
+            if u + v > 1:
+                u, v = 1 - u, 1 - v
+            p = (v0 + u * (v1 - v0) + v * (v2 - v0)).astype(np.float32)
+            n = np.cross(v1 - v0, v2 - v0)
+            n /= np.linalg.norm(n)
+            a = rng.normal(size=3)
+            a -= n * np.dot(a, n)
+            a /= np.linalg.norm(a)
+            el = 10.0 ** rng.uniform(-7, -2) * (1 if rng.random() < 0.5 else -1)
+            w = (a * np.cos(el) + n * np.sin(el)).astype(np.float32)
+            rays.append([*p, *w, 1e-4, 5000.0])
+            flags.append(int(rng.random() < 0.5))
     R = np.ascontiguousarray(np.array(rays, np.float32))
     F = np.ascontiguousarray(np.array(flags, np.uint32))
-    out = np.zeros(30, np.float64)
+    out = np.zeros(50, np.float64)
+    # content boxes of every node's subtree (v3), bottom-up from the leaves' triangles
+    boxes = None
+    if os.environ.get("WALK_BOXES"):
+        n = tree.shape[0]
+        boxes = np.empty((n, 6), np.float32)
+        boxes[:, :3] = np.inf
+        boxes[:, 3:] = -np.inf
+        P3 = pos[:, :3]
+        tb_lo = np.minimum(np.minimum(P3[idx[:, 0]], P3[idx[:, 1]]), P3[idx[:, 2]])
+        tb_hi = np.maximum(np.maximum(P3[idx[:, 0]], P3[idx[:, 1]]), P3[idx[:, 2]])
+        leaf = (tree[:, 0] & 3) == 3
+        for i in np.nonzero(leaf)[0]:
+            c, f = tree[i, 0] >> 2, tree[i, 1]
+            if c:
+                t = ids[f:f + c]
+                boxes[i, :3] = tb_lo[t].min(axis=0)
+                boxes[i, 3:] = tb_hi[t].max(axis=0)
+        for i in range(n - 1, -1, -1):
+            if not leaf[i] and 2 * i + 2 < n:
+                boxes[i, :3] = np.minimum(boxes[2 * i + 1, :3], boxes[2 * i + 2, :3])
+                boxes[i, 3:] = np.maximum(boxes[2 * i + 1, 3:], boxes[2 * i + 2, 3:])
+        # conservative expansion: 2^-k of the scene's coordinate magnitude (WALK_MARGIN_LG, default 14)
+        scale = float(np.abs(pos[:, :3]).max())
+        mg = np.float32(scale * 2.0 ** -float(os.environ.get("WALK_MARGIN_LG", "14")))
+        boxes[:, :3] -= mg
+        boxes[:, 3:] += mg
+        boxes = np.ascontiguousarray(boxes)
     L = lib()
     P = ctypes.c_void_p
     L.walk_sim_levels(int(os.environ.get("WALK_LEVELS", "3")))
+    L.walk_sim_boxes(P(boxes.ctypes.data) if boxes is not None else None)
+    L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
     L.walk_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
                P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
                P(out.ctypes.data))
-    out = out.reshape(3, 10)
+    out = out.reshape(5, 10)
     ks = np.array([4, 6, 8, 10, 12, 16], np.uint32)
     tr = np.zeros(4 * len(ks), np.float64)
     L.trail_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
@@ -85,8 +135,23 @@ def main():
     for k, row in zip(ks, tr):
         print(f"compact trail K={k}: per ray {row[0]:.2f} pushes, {row[1]:.3f} overwrite a pending entry, "
               f"{row[2]:.2f} pops, {row[3]:.3f} pops of a lost entry (recompute)")
+    bad = np.zeros(256)
+    nb = L.walk_sim_bad(P(bad.ctypes.data))
+    for k in range(nb):
+        i, v, t0, tv = bad[4 * k:4 * k + 4]
+        r = R[int(i)]
+        print(f"MISMATCH ray {int(i)} v{int(v)}: v0 tri {int(t0)} vs {int(tv)}; ray {r.tolist()} anyhit {F[int(i)]}")
+        if t0 >= 0:
+            tri = int(t0)
+            vv = pos[idx[tri, :3], :3]
+            print("   v0 hit triangle verts", vv.tolist())
+    if boxes is not None:
+        cu = np.zeros(33)
+        L.walk_sim_culls(P(cu.ctypes.data))
+        print("culls per ray by depth:", {d: round(v / len(R), 3) for d, v in enumerate(cu[:32]) if v},
+              "of which at leaves:", round(cu[32] / len(R), 3))
     print(f"config {cfgn}: {len(R)} rays ({sum(flags)} any-hit), {time.time() - t0:.1f} s")
-    for v in range(3):
+    for v in range(5 if boxes is not None else 3):
         s = {k: round(out[v, i] / len(R), 3) for i, k in enumerate(NAMES)}
         s["mismatch"] = int(out[v, 9])
         tr = out[v, 0] + out[v, 1]
