@@ -795,7 +795,7 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bvh_rec_off = c->bvh_rec_off;
     S.bvh_ids = c->bvh_ids.as<uint32_t>();
     S.bvh_nnodes = c->bvh_nnodes;
-    S.bsp_cull = c->bsp_cull;
+    S.bsp_cull_gap = c->bsp_cull ? 0x1p-18f : INFINITY;
     S.bsp_margin = c->bsp_margin;
     return S;
 }

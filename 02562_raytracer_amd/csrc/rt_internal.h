@@ -38,7 +38,10 @@ struct DevScene {
     uint32_t bvh_rec_off;
     const uint32_t* bvh_ids;
     uint32_t bvh_nnodes;
-    uint32_t bsp_cull;            // the BSP walk skips subtrees whose content box the ray misses (RT_OPT_BSP_CULL)
+    // RT_OPT_BSP_CULL: the BSP walk skips a subtree whose content box the ray misses
+    // by more than this fraction of |tn| + |tf| (2^-18; +inf turns culling off
+    // without a branch on a uniform flag, rt_kernels.hip bsp_box_miss)
+    float bsp_cull_gap;
     float bsp_margin;             // the content boxes' scene margin (rt_kernels.hip bsp_box_miss)
 };
 

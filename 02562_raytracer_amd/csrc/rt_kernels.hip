@@ -593,8 +593,18 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // is skipped.  An axis whose direction component is below the shader's 1e-8
 // cut (inv is then +-1e8 or the NaN flag, see bsp_inv1) constrains nothing: the
 // NaN drops out of fminf / fmaxf.
+// RT_BSP_CULL 0 compiles the test out (A/B builds; RT_OPT_BSP_CULL then has no effect).
+#ifndef RT_BSP_CULL
+#define RT_BSP_CULL 1
+#endif
+// The gap factor `gap` is DevScene.bsp_cull_gap: 2^-18, or +inf with culling
+// off (no gap exceeds an infinite threshold; 0 x inf = NaN compares false).
+// Off is data, not a branch on a uniform flag: a uniform bool kept as a lane
+// mask across the walk loops was reused under a wider exec mask by the
+// compiler (k_direct's shadow walk culled in the lanes that had been inactive
+// where the mask was computed; tests/test_gpu_cull.py caught it).
 __device__ __forceinline__ bool bsp_box_miss(const v4u q0, const v4u q1, const f3 o, const f3 inv, float tmin, float tmax,
-                                             float dscene)
+                                             float dscene, float gap)
 {
     const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
     const float m = __builtin_fmaxf(mo * 0x1p-10f, dscene);
@@ -610,7 +620,7 @@ __device__ __forceinline__ bool bsp_box_miss(const v4u q0, const v4u q1, const f
         tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
     }
     // a clear gap: the rounding of the slab products cannot close it
-    return tn - tf > (rt_absf(tn) + rt_absf(tf)) * 0x1p-18f;
+    return tn - tf > (rt_absf(tn) + rt_absf(tf)) * gap;
 }
 
 // The walking half of a BSP trip: node m (level 0), a child (level 1), a
@@ -626,7 +636,7 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
                                          Counters& c, bool& pop)
 {
     uint32_t m = t.node;
-    if (S.bsp_cull && bsp_box_miss(q0, q1, o, inv, t.tmin, t.tmax, S.bsp_margin)) {
+    if (RT_BSP_CULL && bsp_box_miss(q0, q1, o, inv, t.tmin, t.tmax, S.bsp_margin, S.bsp_cull_gap)) {
         if (COUNT) c.v[C_CULLS]++;
         pop = true;
         return false;
