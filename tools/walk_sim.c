@@ -55,6 +55,8 @@ int g_levels = 3;
 static uint32_t depth_of(uint32_t n0);
 static const float* g_boxes = 0;
 int g_root_only = 0;
+int g_cull_every = 0;
+void walk_sim_cull_every(int c) { g_cull_every = c; }
 double g_bad[256];
 int g_bad_n = 0;
 int walk_sim_bad(double* out) { for (int i = 0; i < 4 * g_bad_n; i++) out[i] = g_bad[i]; return g_bad_n; }
@@ -104,6 +106,11 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
             lv = g_levels;
         }
         while (lv < g_levels) {
+            if (var == 4 && g_cull_every && lv > 0 && box_miss(node, o, d, tmin, tmax)) {
+                do_pop = 1;   /* v4 + WALK_CULL_EVERY: a child's content box too (boxes of every treelet level) */
+                g_cull[depth_of(node) < 32 ? depth_of(node) : 31] += 1;
+                break;
+            }
             const uint32_t* tn = s->tree + 4 * (size_t)node;
             uint32_t ax = tn[0] & 3u;
             if (ax == 3u) {

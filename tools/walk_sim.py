@@ -122,6 +122,7 @@ def main():
     L.walk_sim_levels(int(os.environ.get("WALK_LEVELS", "3")))
     L.walk_sim_boxes(P(boxes.ctypes.data) if boxes is not None else None)
     L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
+    L.walk_sim_cull_every(int(os.environ.get("WALK_CULL_EVERY", "0")))
     L.walk_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
                P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
                P(out.ctypes.data))
