@@ -367,7 +367,9 @@ def main():
             "roofline": roof,
             "cpu_baseline": cpu,
             "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},
-            "traversal_per_launch": {k: detail[k] for k in ("node_interior", "node_leaf", "bvh_pops", "tri_tests",
+            # this rank's counting step: every launch of one step summed (config 5
+            # at 1024 spp is 8 launches of 128 spp, roofline.launches_per_step)
+            "traversal_per_step": {k: detail[k] for k in ("node_interior", "node_leaf", "bvh_pops", "tri_tests",
                                                             "tri_accepts", "trips", "lane_steps",
                                                             "leaf_lane_steps", "node_trips", "leaf_trips",
                                                             "exact_tests", "exact_nodes", "shade_passes",

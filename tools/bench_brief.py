@@ -3,7 +3,7 @@ import json
 import sys
 
 d = json.loads(sys.stdin.read().strip().splitlines()[-1])
-t = d["traversal_per_launch"]
+t = d.get("traversal_per_step") or d["traversal_per_launch"]
 trips = max(1, t["trips"])
 cyc = max(1, t.get("trav_cycles", 0) + t.get("shade_cycles", 0))
 print(f'{d["value"]} Mrays/s  {d["ms_per_step"]} ms/step  kernel {d["roofline"]["kernel_ms"]} ms  '
