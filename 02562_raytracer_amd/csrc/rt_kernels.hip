@@ -1402,7 +1402,12 @@ k_path(DevScene S, DevLaunch L)
     // tails, so finished lanes are refilled early (T_hi); a walk-dominated one
     // (config 3: 0.27, config 4: 0.56) keeps the refills together (T_lo) for
     // the coherence of the pixel-major units.
-    int32_t leaf_score = 0;   // sum of 4 * leaf lanes - 3 * tracing lanes over the checks (wave-uniform)
+    // (T_hi once the leaf share of the tracing lanes reaches NUM/DEN)
+#ifndef RT_THI_SHARE_NUM
+#define RT_THI_SHARE_NUM 3
+#define RT_THI_SHARE_DEN 4
+#endif
+    int32_t leaf_score = 0;   // sum of DEN * leaf lanes - NUM * tracing lanes over the checks (wave-uniform)
     uint64_t tstamp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
         // ---- traversal phase: every tracing lane advances its ray by one node
@@ -1413,7 +1418,7 @@ k_path(DevScene S, DevLaunch L)
             uint32_t Te = T & 0xFFu;
             if (TRAV == RT_TRAVERSE_BSP && (T >> 16)) {   // (the host asks for it on the BSP walk only)
                 const int32_t lf = __popcll(__ballot((st == ST_TRACE) & (tr.leaf_k != tr.leaf_end)));
-                leaf_score += 4 * lf - 3 * (int32_t)__popcll(trm);
+                leaf_score += RT_THI_SHARE_DEN * lf - RT_THI_SHARE_NUM * (int32_t)__popcll(trm);
                 leaf_score = leaf_score < -(1 << 24) ? -(1 << 24) : leaf_score > (1 << 24) ? (1 << 24) : leaf_score;
                 Te = leaf_score >= 0 ? (T >> 8) & 0xFFu : T & 0xFFu;
             }
