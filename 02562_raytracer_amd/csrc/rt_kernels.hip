@@ -1426,14 +1426,18 @@ k_path(DevScene S, DevLaunch L)
     // between T_lo (bits 0-7) and T_hi (bits 8-15) from the share of its
     // tracing lanes that sit in a leaf (testing triangles), counted at every
     // check.  A test-dominated walk (long leaves: config 5's 32-triangle
-    // leaves, 0.83 of the tracing lanes in a leaf) has long, uneven per-lane
-    // tails, so finished lanes are refilled early (T_hi); a walk-dominated one
-    // (config 3: 0.27, config 4: 0.56) keeps the refills together (T_lo) for
-    // the coherence of the pixel-major units.
-    // (T_hi once the leaf share of the tracing lanes reaches NUM/DEN)
+    // leaves; with subtree culling config 4's bunny grid too, 0.73-0.75 of the
+    // tracing lanes in a leaf) has long, uneven per-lane tails, so finished
+    // lanes are refilled early (T_hi); a walk-dominated one (config 3: 0.34)
+    // keeps the refills together (T_lo) for the coherence of the pixel-major
+    // units.
+    // (T_hi once the leaf share of the tracing lanes reaches NUM/DEN: 1/2 since
+    // subtree culling, which made config 4's walk 0.75 and config 5's 0.73 leaf
+    // tests; at 3/4 config 5 ran 2708 vs 2886 Mrays/s at 128 spp, config 4 3521
+    // vs 3559, configs 2 and 3 unchanged; profiles/r03/ab_ls_c*.txt)
 #ifndef RT_THI_SHARE_NUM
-#define RT_THI_SHARE_NUM 3
-#define RT_THI_SHARE_DEN 4
+#define RT_THI_SHARE_NUM 1
+#define RT_THI_SHARE_DEN 2
 #endif
     int32_t leaf_score = 0;   // sum of DEN * leaf lanes - NUM * tracing lanes over the checks (wave-uniform)
     uint64_t tstamp = COUNT ? __builtin_amdgcn_s_memtime() : 0;
