@@ -457,7 +457,7 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 #endif
 // RT_DECIDE_EXACT 1: every decision divides out the exact t (A/B knob)
 #ifndef RT_DECIDE_EXACT
-#define RT_DECIDE_EXACT 0
+#define RT_DECIDE_EXACT 1
 #endif
 template <bool COUNT>
 __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, uint32_t dep, const f3 o,
@@ -547,13 +547,17 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 #ifndef RT_LEAF_TESTS
 #define RT_LEAF_TESTS 2   // triangle tests per leaf trip of the BSP walk: 1 or 2
 #endif
+#ifndef RT_LEAF_PRELOAD
+#define RT_LEAF_PRELOAD 0
+#endif
 template <bool COUNT, bool CULL, class LOG>
-__device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const v4u r1, const f3 o,
-                                               const f3 d, bool anyhit, Trav& t, Counters& c, LOG& lg)
+__device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const v4u r1, const v4u q5,
+                                               const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
     if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
-        // the trip's 80-B load holds this record's first 32 B (nx, r1)
-        const v4u r2 = __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
+        // the trip's 80-B load holds this record's first 32 B (nx, r1); its last
+        // 16 B come with the trip's loads too (RT_LEAF_PRELOAD) or one round trip later
+        const v4u r2 = RT_LEAF_PRELOAD ? q5 : __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
         lg.tested(t.leaf_k);
         if (COUNT) {
             c.v[C_IDS]++;
@@ -581,7 +585,7 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
 // RT_LEAF_TESTS 2, the next one, whose first 16 B are q3).
 template <bool COUNT, bool CULL, class LOG>
 __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, const v4u q0, const v4u q1, const v4u q2,
-                                               const v4u q3, const v4u q4, const f3 o, const f3 d, bool anyhit, Trav& t,
+                                               const v4u q3, const v4u q4, const v4u q5, const f3 o, const f3 d, bool anyhit, Trav& t,
                                                Counters& c, bool& done, bool& pop, LOG& lg)
 {
     lg.tested(t.leaf_k);
@@ -602,7 +606,7 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
         }
     }
     t.leaf_k += 48u;
-    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, q4, o, d, anyhit, t, c, lg);
+    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, q4, q5, o, d, anyhit, t, c, lg);
     const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
     done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
     pop = leaf_done & !t.found;
@@ -712,16 +716,25 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
     v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 48u, 0, 0);
     v4u q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 64u, 0, 0);
-    // keep the five loads together (the compiler would sink the later ones
+    // RT_LEAF_PRELOAD: the second leaf test's last 16 B in the same round trip
+    // (1: every lane loads them, 2: leaf lanes only)
+    v4u q5 = {0u, 0u, 0u, 0u};
+    if (RT_LEAF_PRELOAD == 1 || (RT_LEAF_PRELOAD == 2 && in_leaf))
+        q5 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 80u, 0, 0);
+    // keep the loads together (the compiler would sink the later ones
     // into the level-2 branch: a second round trip)
+#if RT_LEAF_PRELOAD
+    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5));
+#else
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4));
+#endif
     if (COUNT) {   // diagnostics: cycles from issuing the loads to their data
         tw = __builtin_amdgcn_s_memtime() - tw;
         if ((threadIdx.x & 63u) == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u))
             c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
     }
     bool done = false, pop = false;
-    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, o, d, anyhit, t, c, done, pop, lg);
+    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg);
     else bsp_walk<COUNT>(S, stk, q0, q1, q2, q3, q4, o, d, inv, t, c, pop);
     if (pop) done = bsp_pop(stk, t);
     return done;
