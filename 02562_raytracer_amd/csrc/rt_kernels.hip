@@ -17,8 +17,9 @@
 //     gives a refill's lanes the iterations of one pixel (coherent rays);
 //   * ray state machine with ONE traversal call site: each trip every tracing
 //     lane advances its ray (camera / bounce closest-hit, or a shadow any-hit)
-//     by one 64-B load: a treelet walked three BSP levels deep, or a leaf's
-//     triangle records (two tests per trip); lanes whose ray ended wait and
+//     by one 80-B load: a treelet (its subtree's content box, tested first:
+//     subtree culling, then three BSP levels walked), or a leaf's triangle
+//     records (two tests per trip); lanes whose ray ended wait and
 //     shade together once few lanes still trace (shading threshold, chosen
 //     per wave from its leaf share), so no lane waits for the slowest ray;
 //   * per-lane traversal stack in LDS, [level][thread] (conflict-free):
@@ -523,22 +524,25 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 }
 
 // One trip of a lane through intersect_trimesh (bsp.wgsl:10-81).  Every lane
-// issues the same four 16-B loads at one base offset, before any decision
+// issues the same five 16-B loads at one base offset, before any decision
 // (one memory round trip per trip):
-//   * a lane inside a leaf tests one triangle: base = its 48-B record;
-//   * a lane walking nodes reads the 64-B treelet of its node m (rt_api.cpp:
-//     nodes m | 2m, 2m+1 | 4m..4m+3) and walks up to three levels with no
-//     further load.
+//   * a lane inside a leaf tests its 48-B record (and the next one, below);
+//   * a lane walking nodes reads the 80-B treelet of its node m
+//     (rt_bsp_build.hip k_bsp_repack: m's content box | nodes m | 2m, 2m+1 |
+//     4m..4m+3), tests the content box (bsp_walk) and walks up to three
+//     levels with no further load.
 // Treelets and records share one buffer resource (out-of-range reads are 0).
 // A walk that reaches a leaf starts its triangle range (tested from the next
 // trip on); an empty leaf, or a leaf tested without a hit, pops.  Leaf ranges
 // (leaf_k, leaf_end, hit_k) are byte offsets of records in that buffer.
 // A second triangle test of a leaf in the same trip (BSP walk).  A leaf
-// lane's trip loads 64 B at its record: the 48-B record it tests and the
-// first 16 B of the next one (`nx`; records of a leaf are 48 B apart).  The
+// lane's trip loads 80 B at its record: the 48-B record it tests and the
+// first 32 B of the next one (`nx`, `r1`; records of a leaf are 48 B apart).  The
 // next record is tested in order, after the first one's accept has narrowed
-// tmax, exactly as one test per trip would; its other 32 B cost one more
-// round trip.  A walk that stops at its first hit (anyhit) stops here too.
+// tmax, exactly as one test per trip would; its last 16 B cost one more
+// round trip (loading them with the trip's five loads, RT_LEAF_PRELOAD, was no
+// faster: profiles/r03/ab_pre_c*.txt).  A walk that stops at its first hit
+// (anyhit) stops here too.
 // Two tests per trip take the per-trip costs (the check, the walking half of
 // the wave, the pop) off the leaf work: config 3 +2.9 %, config 4 +12 %,
 // config 5 (32-triangle leaves) +20 % (profiles/r02/ab_lt2.txt); three or more
