@@ -462,7 +462,7 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 #endif
 template <bool COUNT>
 __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, uint32_t dep, const f3 o,
-                                               const f3 d, const f3 inv, Trav& t, Counters& c)
+                                               const f3 d, const f3 inv, Trav& t, Counters& c, float lo, float& hi)
 {
     if (COUNT) c.v[C_INTERIOR]++;
     const uint32_t axis = n.x & 3u;
@@ -480,9 +480,11 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
             asm volatile("");   // keep the rare IEEE division behind its branch (no if-conversion)
             tt = x / denom;
         }
-        const bool cnear = tt > t.tmax;
-        const bool gofar = (!cnear) & (tt < t.tmin);
-        const bool push = (!cnear) & !(tt < t.tmin);
+        // against [lo, hi]: the ray interval, clipped to the treelet root's
+        // content box (RT_BSP_CLIP); a plane beyond it leaves one side hitless
+        const bool cnear = tt > hi;
+        const bool gofar = (!cnear) & (tt < lo);
+        const bool push = (!cnear) & !(tt < lo);
         if (RT_TRAIL_SLOT) {
             stk[0] = t.tmax;
             t.lvl |= (uint32_t)push << dep;
@@ -491,6 +493,7 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
             t.lvl |= push ? 1u << dep : 0u;
         }
         t.tmax = push ? tt : t.tmax;
+        hi = push ? tt : hi;
         return gofar ? near_node ^ 1u : near_node;
     }
     const float tq = x * iv;
@@ -633,6 +636,11 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 #ifndef RT_BSP_CULL
 #define RT_BSP_CULL 1
 #endif
+// RT_BSP_CLIP 1: the trip's decisions also use the interval clipped to the box
+// (bsp_walk; DESIGN.md section 4 "Subtree culling")
+#ifndef RT_BSP_CLIP
+#define RT_BSP_CLIP 1
+#endif
 // The gap factor `gap` is DevScene.bsp_cull_gap: 2^-18, or +inf with culling
 // off (no gap exceeds an infinite threshold; 0 x inf = NaN compares false).
 // Off is data, not a branch on a uniform flag: a uniform bool kept as a lane
@@ -640,7 +648,7 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // compiler (k_direct's shadow walk culled in the lanes that had been inactive
 // where the mask was computed; tests/test_gpu_cull.py caught it).
 __device__ __forceinline__ bool bsp_box_miss(const v4u q0, const v4u q1, const f3 o, const f3 inv, float tmin, float tmax,
-                                             float dscene, float gap)
+                                             float dscene, float gap, float& lo, float& hi)
 {
     const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
     const float m = __builtin_fmaxf(mo * 0x1p-10f, dscene);
@@ -656,7 +664,12 @@ __device__ __forceinline__ bool bsp_box_miss(const v4u q0, const v4u q1, const f
         tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
     }
     // a clear gap: the rounding of the slab products cannot close it
-    return tn - tf > (rt_absf(tn) + rt_absf(tf)) * gap;
+    const float e = (rt_absf(tn) + rt_absf(tf)) * gap;
+    // the interval the subtree's content can be hit in, widened by the same
+    // tolerance (RT_BSP_CLIP; culling off: e = inf or NaN, lo = tmin, hi = tmax)
+    lo = __builtin_fmaxf(tmin, tn - e);
+    hi = __builtin_fminf(tmax, tf + e);
+    return tn - tf > e;
 }
 
 // The walking half of a BSP trip: node m (level 0), a child (level 1), a
@@ -672,10 +685,18 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
                                          Counters& c, bool& pop)
 {
     uint32_t m = t.node;
-    if (RT_BSP_CULL && bsp_box_miss(q0, q1, o, inv, t.tmin, t.tmax, S.bsp_margin, S.bsp_cull_gap)) {
-        if (COUNT) c.v[C_CULLS]++;
-        pop = true;
-        return false;
+    float lo = t.tmin, hi = t.tmax;   // the decisions' interval
+    if (RT_BSP_CULL) {
+        float blo, bhi;
+        if (bsp_box_miss(q0, q1, o, inv, t.tmin, t.tmax, S.bsp_margin, S.bsp_cull_gap, blo, bhi)) {
+            if (COUNT) c.v[C_CULLS]++;
+            pop = true;
+            return false;
+        }
+        if (RT_BSP_CLIP) {
+            lo = blo;
+            hi = bhi;
+        }
     }
     const uint32_t dep = heap_depth(m);
     uint2 n = make_uint2(q1.z, q1.w);
@@ -683,15 +704,15 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
     if (!leaf) {
         // the trail slot of this level (RT_TRAIL_SLOT), or the trail base
         float* const s0 = RT_TRAIL_SLOT ? stk + dep * 256u : stk;
-        m = bsp_decide<COUNT>(s0, n, m, dep, o, d, inv, t, c);
+        m = bsp_decide<COUNT>(s0, n, m, dep, o, d, inv, t, c, lo, hi);
         n = (m & 1u) ? make_uint2(q2.z, q2.w) : make_uint2(q2.x, q2.y);
         leaf = (n.x & 3u) == 3u;
         if (!leaf) {
-            m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 256 : stk, n, m, dep + 1u, o, d, inv, t, c);
+            m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 256 : stk, n, m, dep + 1u, o, d, inv, t, c, lo, hi);
             const v4u g = (m & 2u) ? q4 : q3;
             n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
             leaf = (n.x & 3u) == 3u;
-            if (!leaf) m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 512 : stk, n, m, dep + 2u, o, d, inv, t, c);
+            if (!leaf) m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 512 : stk, n, m, dep + 2u, o, d, inv, t, c, lo, hi);
         }
     }
     t.node = m;

@@ -56,6 +56,11 @@ static uint32_t depth_of(uint32_t n0);
 static const float* g_boxes = 0;
 int g_root_only = 0;
 int g_cull_every = 0;
+int g_clip = 0;
+int g_chunk = 0, g_chunk_min = 0, g_chunk_free = 0;
+float g_chunk_margin = 0;
+void walk_sim_chunk(int c, int mn, int fr, float mg) { g_chunk = c; g_chunk_min = mn; g_chunk_free = fr; g_chunk_margin = mg; }
+void walk_sim_clip(int c) { g_clip = c; }
 void walk_sim_cull_every(int c) { g_cull_every = c; }
 double g_bad[256];
 int g_bad_n = 0;
@@ -64,9 +69,12 @@ double g_cull[32], g_cull_leaf;
 void walk_sim_culls(double* out) { for (int i = 0; i < 32; i++) out[i] = g_cull[i]; out[32] = g_cull_leaf; }
 void walk_sim_root_only(int r) { g_root_only = r; }   /* nnodes x 6: content box (min.xyz, max.xyz) of each node's subtree, or NULL */
 void walk_sim_boxes(const float* b) { g_boxes = b; }
+static float g_tn, g_tf;   /* the ray interval clipped to the last tested box */
 static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
 {
     const float* b = g_boxes + 6 * (size_t)node;
+    g_tn = tmin;
+    g_tf = tmax;
     if (b[0] > b[3]) return 1;   /* empty subtree */
     float t0 = tmin, t1 = tmax;
     for (int k = 0; k < 3; k++) {
@@ -77,6 +85,8 @@ static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
         if (a > t0) t0 = a;
         if (c < t1) t1 = c;
     }
+    g_tn = t0;
+    g_tf = t1;
     return t0 > t1;
 }
 void walk_sim_levels(int l) { g_levels = l; }
@@ -99,11 +109,15 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
         /* one walking trip from `node`: up to three levels */
         st[S_WT] += 1;
         int lv = 0, reached_leaf = 0, do_pop = 0;
+        float ctn = -INFINITY, ctf = INFINITY;   /* v4 + WALK_CLIP: decisions against the box's interval */
         if (var >= 3 && g_boxes && (node == 0 || !g_root_only) && box_miss(node, o, d, tmin, tmax)) {
             do_pop = 1;   /* v3: the subtree's content misses the ray interval */
             g_cull[depth_of(node) < 32 ? depth_of(node) : 31] += 1;
             g_cull_leaf += (s->tree[4 * node] & 3u) == 3u;
             lv = g_levels;
+        } else if (var == 4 && g_boxes && g_clip) {
+            ctn = g_tn;
+            ctf = g_tf;
         }
         while (lv < g_levels) {
             if (var == 4 && g_cull_every && lv > 0 && box_miss(node, o, d, tmin, tmax)) {
@@ -123,6 +137,28 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
                     /* leaf trips: two tests per trip */
                     uint32_t j = 0;
                     while (j < cnt) {
+                        if (var == 4 && g_chunk && j % (uint32_t)g_chunk == 0 && cnt > (uint32_t)g_chunk_min) {
+                            /* v4 + WALK_CHUNK: a header trip tests the box of the next
+                             * g_chunk records (in leaf order) and skips them on a miss */
+                            uint32_t e = j + (uint32_t)g_chunk < cnt ? j + (uint32_t)g_chunk : cnt;
+                            float bb[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+                            for (uint32_t q = j; q < e; q++) {
+                                const uint32_t* ix = s->idx + 4 * (size_t)s->ids[first + q];
+                                for (int vv = 0; vv < 3; vv++)
+                                    for (int a = 0; a < 3; a++) {
+                                        float x = s->pos[4 * ix[vv] + a];
+                                        if (x < bb[a]) bb[a] = x;
+                                        if (x > bb[3 + a]) bb[3 + a] = x;
+                                    }
+                            }
+                            for (int a = 0; a < 3; a++) { bb[a] -= g_chunk_margin; bb[3 + a] += g_chunk_margin; }
+                            st[S_LT] += g_chunk_free ? 0 : 1;
+                            const float* sv = g_boxes;
+                            g_boxes = bb;
+                            int miss = box_miss(0, o, d, tmin, tmax);
+                            g_boxes = sv;
+                            if (miss) { j = e; continue; }
+                        }
                         st[S_LT] += 1;
                         for (int k = 0; k < 2 && j < cnt; k++, j++) {
                             float dd;
@@ -147,9 +183,9 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
             uint32_t nearn = ad >= 0.0f ? tn[2] : tn[3], farn = ad >= 0.0f ? tn[3] : tn[2];
             float den = fabsf(ad) < 1.0e-8f ? 1.0e-8f : ad;
             float t = (s->planes[node] - ao) / den;
-            if (t > tmax) {
+            if (t > tmax || t > ctf) {
                 node = nearn;
-            } else if (t < tmin) {
+            } else if (t < tmin || t < ctn) {
                 node = farn;
             } else if ((var == 1 || var == 2 || var == 3) && is_empty_leaf(s, nearn)) {
                 /* push + visit the empty near leaf + pop, folded: the counted

@@ -123,6 +123,11 @@ def main():
     L.walk_sim_boxes(P(boxes.ctypes.data) if boxes is not None else None)
     L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
     L.walk_sim_cull_every(int(os.environ.get("WALK_CULL_EVERY", "0")))
+    L.walk_sim_clip(int(os.environ.get("WALK_CLIP", "0")))
+    L.walk_sim_chunk.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float]
+    L.walk_sim_chunk(int(os.environ.get("WALK_CHUNK", "0")), int(os.environ.get("WALK_CHUNK_MIN", "0")),
+                     int(os.environ.get("WALK_CHUNK_FREE", "0")),
+                     float(np.abs(pos[:, :3]).max()) * 2.0 ** -float(os.environ.get("WALK_MARGIN_LG", "14")))
     L.walk_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
                P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
                P(out.ctypes.data))
