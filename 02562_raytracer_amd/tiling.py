@@ -1,5 +1,6 @@
 """Framebuffer tiling across ranks: one process per GPU, each
-renders the interleaved 8x8 tiles t = l*nranks + rank (rt_render_tiles), the
+renders the interleaved 8x8 tiles at sequence positions s = l*nranks + rank
+(rt_render_tiles; tile_of_seq: rows rotated by their index), the
 packed tiles are gathered to rank 0, and rank 0 scatters them into the frame
 (rt_unpack_tiles).  The gather is the only collective of the path.
 
@@ -17,6 +18,14 @@ def tile_grid(width, height):
     return (width + TILE - 1) // TILE, (height + TILE - 1) // TILE
 
 
+def tile_of_seq(s, tx_n):
+    """Tile (tx, ty) at sequence position s (include/rt.h rt_tileset): row-major,
+    each row rotated by its index, so the ranks' tiles (s % nranks) form diagonal
+    stripes instead of whole columns when nranks divides the tile columns."""
+    ty = s // tx_n
+    return (s % tx_n + ty % tx_n) % tx_n, ty
+
+
 def packed_pixel_coords(width, height, rank, nranks, local_tiles):
     """Global (x, y) of every packed pixel of `rank`, and whether it is inside
     the frame -- the mapping k_path / k_primary use in tileset mode."""
@@ -24,8 +33,9 @@ def packed_pixel_coords(width, height, rank, nranks, local_tiles):
     lane = np.arange(64)
     l = np.arange(local_tiles)[:, None]
     t = l * nranks + rank
-    x = (t % tx_n) * TILE + (lane & 7)[None, :]
-    y = (t // tx_n) * TILE + (lane >> 3)[None, :]
+    tx, ty = tile_of_seq(t, tx_n)
+    x = tx * TILE + (lane & 7)[None, :]
+    y = ty * TILE + (lane >> 3)[None, :]
     valid = (t < tx_n * ty_n) & (x < width) & (y < height)
     return x.reshape(-1), y.reshape(-1), valid.reshape(-1)
 

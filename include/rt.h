@@ -115,9 +115,12 @@ typedef struct rt_tile {
 } rt_tile;
 
 /* Interleaved 8x8-tile partition of the full frame for multi-GPU rendering
- * (SURVEY.md 8(e)): tile t (row-major over ceil(W/8) x ceil(H/8) tiles) is owned
- * by rank t % nranks.  Global pixel coordinates keep PRNG seeds, and therefore
- * images, identical for every nranks. */
+ * (SURVEY.md 8(e)): the tiles (ceil(W/8) x ceil(H/8)) are taken in sequence
+ * s = ty * tiles_x + (tx - ty) mod tiles_x -- row-major, each row rotated by its
+ * index -- and sequence position s is owned by rank s % nranks (diagonal
+ * stripes: when nranks divides tiles_x, rank r owns tx = r + ty mod nranks).
+ * Global pixel coordinates keep PRNG seeds, and therefore images, identical
+ * for every nranks. */
 typedef struct rt_tileset {
     uint32_t rank;
     uint32_t nranks;
@@ -337,8 +340,8 @@ int rt_render(rt_ctx* ctx, rt_mode mode, rt_traverse trav, const rt_tile* region
               rt_ray_counts* counts);
 
 /* Same, over the 8x8 tiles owned by `ts` (multi-GPU framebuffer tiling).
- * Outputs are PACKED: local tile l (the l-th tile with t % nranks == rank,
- * i.e. global tile t = l*nranks + rank) occupies pixels [l*64, l*64+64),
+ * Outputs are PACKED: local tile l (the tile at sequence position
+ * s = l*nranks + rank, rt_tileset above) occupies pixels [l*64, l*64+64),
  * row-major inside the tile.  Buffers hold rt_tileset_local_tiles() * 64 px. */
 int rt_render_tiles(rt_ctx* ctx, rt_mode mode, rt_traverse trav, const rt_tileset* ts,
                     uint32_t first_iter, uint32_t spp,

@@ -42,8 +42,8 @@ def _render_rank(rank, nranks, lt):
     ids = np.full((lt * 64,), 0xFFFFFFFF, np.uint32)
     tx_n, _ = tiling.tile_grid(W, H)
     for l in range(lt):
-        t = l * nranks + rank
-        x0, y0 = (t % tx_n) * 8, (t // tx_n) * 8
+        tx, ty = tiling.tile_of_seq(l * nranks + rank, tx_n)
+        x0, y0 = tx * 8, ty * 8
         if y0 >= H:
             continue
         w, h = min(8, W - x0), min(8, H - y0)
