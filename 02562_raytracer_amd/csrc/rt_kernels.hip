@@ -211,10 +211,12 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
         p.out = ry * L.w + rx;
     } else {
         // sequence position s = work * nranks + rank; row ty = s / tiles_x, the
-        // row rotated by ty (tile_of_seq): rank r owns the diagonal columns
-        // tx = r + ty (mod nranks) when nranks divides tiles_x (1080p: 240)
+        // row rotated by ty mod 8 (tiling.tile_of_seq): rank r owns the diagonal
+        // columns tx = r + ty (mod nranks) when nranks divides 8 and tiles_x
+        // (1080p: 240 tile columns); frames under 8 tiles wide are not rotated
         uint32_t t = work * L.nranks + L.rank;
-        uint32_t ty = t / tiles_x, tx = (t % tiles_x + ty % tiles_x) % tiles_x;
+        uint32_t ty = t / tiles_x, tx = t - ty * tiles_x + (tiles_x >= 8u ? (ty & 7u) : 0u);
+        tx = tx >= tiles_x ? tx - tiles_x : tx;
         p.x = tx * 8u + lx;
         p.y = ty * 8u + ly;
         p.valid = (t < L.tiles_x * L.tiles_y) && p.x < L.u.resolution[0] && p.y < L.u.resolution[1];
@@ -228,8 +230,8 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
 __device__ __forceinline__ uint32_t pixel_out(const DevLaunch& L, uint32_t x, uint32_t y)
 {
     if (L.tileset == 0) return (y - L.y0) * L.w + (x - L.x0);
-    const uint32_t ty = y >> 3, tx = x >> 3;
-    const uint32_t t = ty * L.tiles_x + (tx + L.tiles_x - ty % L.tiles_x) % L.tiles_x;   // map_pixel's s
+    const uint32_t ty = y >> 3, tx = x >> 3, r = L.tiles_x >= 8u ? (ty & 7u) : 0u;
+    const uint32_t t = ty * L.tiles_x + (tx >= r ? tx - r : tx + L.tiles_x - r);   // map_pixel's s
     return (t - L.rank) / L.nranks * 64u + ((y & 7u) << 3) + (x & 7u);
 }
 // The work shard of this wave: the XCD it runs on (HW_REG_XCC_ID, hwreg 20,
@@ -2469,9 +2471,11 @@ __global__ void __launch_bounds__(256) k_unpack(uint32_t W, uint32_t H, uint32_t
     const uint64_t total = (uint64_t)tiles_x * tiles_y * 64u;
     for (uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; g < total;
          g += (uint64_t)gridDim.x * blockDim.x) {
-        // t: the sequence position (map_pixel: rows rotated by their index)
+        // t: the sequence position (map_pixel: rows rotated by their index mod 8)
         const uint32_t t = (uint32_t)(g >> 6), lane = (uint32_t)(g & 63u);
-        const uint32_t ty = t / tiles_x, tx = (t % tiles_x + ty % tiles_x) % tiles_x;
+        const uint32_t ty = t / tiles_x;
+        uint32_t tx = t - ty * tiles_x + (tiles_x >= 8u ? (ty & 7u) : 0u);
+        tx = tx >= tiles_x ? tx - tiles_x : tx;
         const uint32_t x = tx * 8u + (lane & 7u), y = ty * 8u + (lane >> 3);
         if (x >= W || y >= H) continue;
         const uint32_t rank = t % nranks, l = t / nranks;

@@ -1,6 +1,6 @@
 """Framebuffer tiling across ranks: one process per GPU, each
 renders the interleaved 8x8 tiles at sequence positions s = l*nranks + rank
-(rt_render_tiles; tile_of_seq: rows rotated by their index), the
+(rt_render_tiles; tile_of_seq: rows rotated by their index mod 8), the
 packed tiles are gathered to rank 0, and rank 0 scatters them into the frame
 (rt_unpack_tiles).  The gather is the only collective of the path.
 
@@ -20,10 +20,12 @@ def tile_grid(width, height):
 
 def tile_of_seq(s, tx_n):
     """Tile (tx, ty) at sequence position s (include/rt.h rt_tileset): row-major,
-    each row rotated by its index, so the ranks' tiles (s % nranks) form diagonal
-    stripes instead of whole columns when nranks divides the tile columns."""
+    each row rotated by its index mod 8 (frames under 8 tiles wide: not rotated),
+    so the ranks' tiles (s % nranks) form diagonal stripes instead of whole
+    columns when nranks divides 8 and the tile columns."""
     ty = s // tx_n
-    return (s % tx_n + ty % tx_n) % tx_n, ty
+    r = (ty & 7) if tx_n >= 8 else 0 * ty
+    return (s % tx_n + r) % tx_n, ty
 
 
 def packed_pixel_coords(width, height, rank, nranks, local_tiles):

@@ -116,9 +116,10 @@ typedef struct rt_tile {
 
 /* Interleaved 8x8-tile partition of the full frame for multi-GPU rendering
  * (SURVEY.md 8(e)): the tiles (ceil(W/8) x ceil(H/8)) are taken in sequence
- * s = ty * tiles_x + (tx - ty) mod tiles_x -- row-major, each row rotated by its
- * index -- and sequence position s is owned by rank s % nranks (diagonal
- * stripes: when nranks divides tiles_x, rank r owns tx = r + ty mod nranks).
+ * s = ty * tiles_x + (tx - (ty & 7)) mod tiles_x -- row-major, each row rotated
+ * by its index mod 8 (not rotated when tiles_x < 8) -- and sequence position s
+ * is owned by rank s % nranks (diagonal stripes: when nranks divides 8 and
+ * tiles_x, rank r owns tx = r + ty mod nranks).
  * Global pixel coordinates keep PRNG seeds, and therefore images, identical
  * for every nranks. */
 typedef struct rt_tileset {
