@@ -54,7 +54,8 @@ struct DevLaunch {
     const uint32_t* env_tex;      // RGBA8 equirectangular hdri0, or null for the constant env
     uint32_t env_w, env_h;
     // region mode (tileset == 0): 8x8 tiles over [x0,x0+w) x [y0,y0+h), row-major region output
-    // tileset mode (tileset == 1): global 8x8 tiles t = l*nranks + rank, packed output
+    // tileset mode (tileset == 1): the 8x8 tile at sequence position s = l*nranks + rank
+    // (rt.h rt_tileset: rows rotated by their index mod 8), packed output
     uint32_t tileset;
     uint32_t x0, y0, w, h;
     uint32_t rank, nranks;
