@@ -863,14 +863,14 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // BVH 2-4 best, 4695 vs 4604 Mrays/s at 8)
     // defaults per walk and shader (profiles/r02/ab_w7e3_shards.txt: W7E3's short
     // Cornell-box rays shade often, and refilling earlier pays there)
-    // The BSP walk of the other modes chooses per wave between 8 and 32 (bit 16:
-    // adaptive, k_path "Shading threshold"): 8 for walk-dominated scenes (configs
-    // 3, 4), 32 for test-dominated ones (config 5's 32-triangle leaves;
-    // profiles/r02/sweep_T_r2final.txt).
+    // The BSP walk of the other modes chooses per wave between 8 and 24 (bit 16:
+    // adaptive, k_path "Shading threshold"): 8 for walk-dominated scenes (config
+    // 3), 24 for test-dominated ones (configs 4 and 5 since subtree culling; fixed
+    // thresholds 12..48 on them: 24 best, profiles/r03/ab_T{hi,lo}_c{4,5}.txt).
     L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold
                                    : trav == RT_TRAVERSE_BVH ? 4
                                    : mode == RT_MODE_W7E3    ? 24
-                                                             : (1u << 16) | (32u << 8) | 8u);
+                                                             : (1u << 16) | (24u << 8) | 8u);
     L.reserved0 = 0;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
