@@ -64,8 +64,8 @@ struct rt_ctx {
     int shade_threshold = -1;   // -1: per walk (BSP 8, BVH 4); pixel-major units refill together (coherent samples)
     uint32_t sample_chunk = 1;          // iterations per k_path work unit
     uint32_t unit_order = 1;            // 0: chunk-major, 1: pixel-major
-    uint32_t bsp_cull = 1;              // RT_OPT_BSP_CULL: subtree culling by content boxes in the BSP walk
-    float bsp_margin = 0.0f;            // its scene margin: 2^-10 x the scene's coordinate magnitude (set on upload)
+    uint32_t bsp_cull = RT_BSP_CULL_CERTIFIED;   // RT_OPT_BSP_CULL: subtree culling by content boxes in the BSP walk
+    float bsp_scale = 0.0f;             // the scene's coordinate magnitude (set on upload; the margins' scale)
     uint64_t sample_budget_mb = 16384;  // per-sample scratch (one pass at 1080p x 256 spp needs 8.1 GiB)
     DevBuf samples;
     bool detail = false;
@@ -274,7 +274,8 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
         c->ktiming = value != 0;
         return RT_OK;
     case RT_OPT_BSP_CULL:
-        if (value < 0 || value > 1) return fail(c, RT_E_INVALID, "BSP cull must be 0 or 1");
+        if (value < RT_BSP_CULL_OFF || value > RT_BSP_CULL_FAST)
+            return fail(c, RT_E_INVALID, "BSP cull must be RT_BSP_CULL_OFF, _CERTIFIED or _FAST");
         c->bsp_cull = (uint32_t)value;
         return RT_OK;
     case RT_OPT_UNIT_ORDER:
@@ -423,13 +424,13 @@ int rt_upload_mesh(rt_ctx* c, const float* pos_vec4, const float* nrm_vec4, uint
 // The traversal layout of the context's BSP (reference arrays already in
 // bsp_ref_tree / bsp_ref_planes / bsp_ids, mesh in pos / idx): content boxes,
 // 80-B treelets and the 48-B records (rt_bsp_build.hip launch_bsp_repack), and
-// the content boxes' scene margin: 2^-10 of the largest coordinate magnitude of
+// the scale of the content boxes' margins: the largest coordinate magnitude of
 // the BSP's root box (bsp_box_miss in rt_kernels.hip adds the ray origin's).
 static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off, size_t total, const float aabb[8])
 {
     HIPCHK(c, c->bsp_nodes.alloc(total));
     DevBuf boxes;
-    HIPCHK(c, boxes.alloc((size_t)nnodes * 32));
+    HIPCHK(c, boxes.alloc((size_t)nnodes * 64));
     if (rtk::launch_bsp_repack(c->bsp_ref_tree.as<uint32_t>(), c->bsp_ref_planes.as<float>(), nnodes,
                                (uint32_t)rec_off, c->bsp_nodes.p, c->pos.as<float4>(), c->idx.as<uint4>(),
                                c->bsp_ids.as<uint32_t>(), nids, 0.0f, boxes.p, c->stream))
@@ -438,7 +439,7 @@ static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off,
     float scale = 0.0f;
     for (int k : {0, 1, 2, 4, 5, 6})
         if (std::isfinite(aabb[k])) scale = std::max(scale, std::fabs(aabb[k]));
-    c->bsp_margin = std::ldexp(scale, -10);
+    c->bsp_scale = scale;
     return RT_OK;
 }
 
@@ -795,8 +796,19 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bvh_rec_off = c->bvh_rec_off;
     S.bvh_ids = c->bvh_ids.as<uint32_t>();
     S.bvh_nnodes = c->bvh_nnodes;
-    S.bsp_cull_gap = c->bsp_cull ? 0x1p-18f : INFINITY;
-    S.bsp_margin = c->bsp_margin;
+    // the culling margin as data (rt_internal.h DevScene, rt_kernels.hip bsp_box_miss)
+    S.bsp_cull_gap = c->bsp_cull != RT_BSP_CULL_OFF ? 0x1p-18f : INFINITY;
+    if (c->bsp_cull == RT_BSP_CULL_FAST) {
+        S.cull_k1 = 0.0f;
+        S.cull_k3 = 0.0f;
+        S.cull_ko = 0x1p-10f;
+        S.bsp_margin = std::ldexp(c->bsp_scale, -10);
+    } else {
+        S.cull_k1 = 36.0f * 0x1p-24f;
+        S.cull_k3 = 2.0f * 0x1p-24f;
+        S.cull_ko = 0x1p-19f;
+        S.bsp_margin = std::ldexp(c->bsp_scale, -19);
+    }
     return S;
 }
 

@@ -23,6 +23,7 @@
 // scan.  Node slots are fixed by (depth, branch) (idx = 2^depth + branch - 1),
 // so only the first ids depend on DFS order.
 // Numerics: the same f32 expressions as the host builder, -ffp-contract=off.
+#include <hip/hip_fp16.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -438,20 +439,30 @@ __global__ void __launch_bounds__(256) k_leaf_finish(const Leaf* leaves, const u
 
 namespace rtk {
 
-// rt_upload_bsp's repack on device: the 64-B treelet of every 1-based node M
-// (nodes M, 2M, 2M+1, 4M..4M+3 as 8-B entries) and the 48-B triangle records.
+// rt_upload_bsp's repack on device: the 96-B treelet of every 1-based node M
+// (M's content box and certification data, nodes M, 2M, 2M+1, 4M..4M+3 as 8-B
+// entries) and the 48-B triangle records.
 // Content box of every node's subtree: the union of the bounding boxes of the
 // triangles its leaves reference (2 x float4 per node: min, max; empty: +inf /
 // -inf).  The BSP walk skips a subtree whose box the ray interval misses
 // (rt_kernels.hip bsp_walk, DESIGN.md section 4 "Subtree culling").
+// Certification data of every node's subtree (2 x float4 per node), for the
+// certified margin of bsp_box_miss (DESIGN.md section 4 "Certified culling"):
+//   {E2, nlo.xyz}, {0, nhi.xyz}: E2 = the largest max(|e0|inf, |e1|inf)^2 over
+//   its triangles (e0, e1: the records' f32 edges), [nlo, nhi] = a box holding
+//   every triangle's exact normal n* = e0 x e1 (rounded outward to f32).
 // Leaves first (a leaf range outside ids -- an unreachable node -- stays empty),
 // then the interior nodes one depth at a time, bottom-up.
+__device__ __forceinline__ float f_rd(double x) { return __double2float_rd(x); }
+__device__ __forceinline__ float f_ru(double x) { return __double2float_ru(x); }
 __global__ void __launch_bounds__(256) k_leaf_boxes(const uint32_t* tree, uint32_t nnodes, const float4* pos,
-                                                    const uint4* idx, const uint32_t* ids, uint32_t nids, float4* box)
+                                                    const uint4* idx, const uint32_t* ids, uint32_t nids, float4* box,
+                                                    float4* cert)
 {
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nnodes; i += gridDim.x * 256u) {
         const uint32_t n0 = tree[4 * (size_t)i], first = tree[4 * (size_t)i + 1];
         float4 lo = make_float4(INFINITY, INFINITY, INFINITY, 0.0f), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, 0.0f);
+        float4 c0 = make_float4(0.0f, INFINITY, INFINITY, INFINITY), c1 = make_float4(0.0f, -INFINITY, -INFINITY, -INFINITY);
         const uint32_t cnt = (n0 & 3u) == 3u ? n0 >> 2 : 0u;
         if ((uint64_t)first + cnt <= nids) {
             for (uint32_t k = 0; k < cnt; k++) {
@@ -465,33 +476,67 @@ __global__ void __launch_bounds__(256) k_leaf_boxes(const uint32_t* tree, uint32
                     hi.y = fmaxf(hi.y, v[j].y);
                     hi.z = fmaxf(hi.z, v[j].z);
                 }
+                // the record's f32 edges (k_tri_records2) and their exact cross
+                // product: the f32 products are exact in f64, the differences
+                // carry a 2^-53 relative error, covered by the outward rounding
+                const float e0[3] = {v[1].x - v[0].x, v[1].y - v[0].y, v[1].z - v[0].z};
+                const float e1[3] = {v[2].x - v[0].x, v[2].y - v[0].y, v[2].z - v[0].z};
+                const double n[3] = {(double)e0[1] * e1[2] - (double)e0[2] * e1[1],
+                                     (double)e0[2] * e1[0] - (double)e0[0] * e1[2],
+                                     (double)e0[0] * e1[1] - (double)e0[1] * e1[0]};
+                const double E = fmax(fmax(fmax(fabs((double)e0[0]), fabs((double)e0[1])), fabs((double)e0[2])),
+                                      fmax(fmax(fabs((double)e1[0]), fabs((double)e1[1])), fabs((double)e1[2])));
+                c0.x = fmaxf(c0.x, f_ru(E * E));
+                const double sl = 0x1p-50;
+                c0.y = fminf(c0.y, f_rd(n[0] - fabs(n[0]) * sl));
+                c0.z = fminf(c0.z, f_rd(n[1] - fabs(n[1]) * sl));
+                c0.w = fminf(c0.w, f_rd(n[2] - fabs(n[2]) * sl));
+                c1.y = fmaxf(c1.y, f_ru(n[0] + fabs(n[0]) * sl));
+                c1.z = fmaxf(c1.z, f_ru(n[1] + fabs(n[1]) * sl));
+                c1.w = fmaxf(c1.w, f_ru(n[2] + fabs(n[2]) * sl));
             }
         }
         box[2 * (size_t)i] = lo;
         box[2 * (size_t)i + 1] = hi;
+        cert[2 * (size_t)i] = c0;
+        cert[2 * (size_t)i + 1] = c1;
     }
 }
 __global__ void __launch_bounds__(256) k_node_boxes(const uint32_t* tree, uint32_t nnodes, uint32_t lo_i, uint32_t hi_i,
-                                                    float4* box)
+                                                    float4* box, float4* cert)
 {
     for (uint32_t i = lo_i + blockIdx.x * 256u + threadIdx.x; i < hi_i; i += gridDim.x * 256u) {
         if ((tree[4 * (size_t)i] & 3u) == 3u || 2ull * i + 2 >= nnodes) continue;   // a leaf (done) / no children
-        const float4 a0 = box[2 * (2 * (size_t)i + 1)], a1 = box[2 * (2 * (size_t)i + 1) + 1];
-        const float4 b0 = box[2 * (2 * (size_t)i + 2)], b1 = box[2 * (2 * (size_t)i + 2) + 1];
+        const size_t l = 2 * (2 * (size_t)i + 1), r = 2 * (2 * (size_t)i + 2);
+        const float4 a0 = box[l], a1 = box[l + 1], b0 = box[r], b1 = box[r + 1];
         box[2 * (size_t)i] = make_float4(fminf(a0.x, b0.x), fminf(a0.y, b0.y), fminf(a0.z, b0.z), 0.0f);
         box[2 * (size_t)i + 1] = make_float4(fmaxf(a1.x, b1.x), fmaxf(a1.y, b1.y), fmaxf(a1.z, b1.z), 0.0f);
+        const float4 p0 = cert[l], p1 = cert[l + 1], q0 = cert[r], q1 = cert[r + 1];
+        cert[2 * (size_t)i] = make_float4(fmaxf(p0.x, q0.x), fminf(p0.y, q0.y), fminf(p0.z, q0.z), fminf(p0.w, q0.w));
+        cert[2 * (size_t)i + 1] = make_float4(0.0f, fmaxf(p1.y, q1.y), fmaxf(p1.z, q1.z), fmaxf(p1.w, q1.w));
     }
 }
 
-// The 80-B treelet of 1-based node M at 80*M (rt_internal.h BSP_TREELET_BYTES):
-// {box min.xyz, max.x | max.y, max.z, node M | nodes 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3}
-// -- node M's content box, expanded by `margin` on every side, and the 8-B
-// nodes a three-level walk from M reads (interior {axis, plane bits}; leaf
-// {3 | (48*count) << 2, byte offset of its first record}).
+// f16 bits of x rounded toward -inf (down) or +inf (up)
+__device__ __forceinline__ uint32_t h_rd(float x) { return __half_as_ushort(__float2half_rd(x)); }
+__device__ __forceinline__ uint32_t h_ru(float x) { return __half_as_ushort(__float2half_ru(x)); }
+
+// The 96-B treelet of 1-based node M at 96*M (rt_internal.h BSP_TREELET_BYTES):
+// {box min.xyz, max.x | max.y, max.z, node M | nodes 2M, 2M+1 | 4M, 4M+1 |
+//  4M+2, 4M+3 | F, c.xy, c.z r.x, r.yz}
+// -- node M's content box, expanded by `margin` on every side, the 8-B nodes a
+// three-level walk from M reads (interior {axis, plane bits}; leaf {3 |
+// (48*count) << 2, byte offset of its first record}), and the certification
+// data: F = 1e-10 / E2 rounded down (+inf for a subtree without a triangle of
+// non-zero extent), and the normal box divided by E2 (|x| <= 2: |n*_i| <=
+// 2 E2) as its centre c (f16, nearest) and radius r (f16, rounded up, so that
+// the box lies inside [c - r, c + r]).
 __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes,
-                                                    uint32_t rec_off, const float4* box, float margin, uint32_t* tl)
+                                                    uint32_t rec_off, const float4* box, const float4* cert,
+                                                    float margin, uint32_t* tl)
 {
     const size_t slots = (size_t)nnodes + 1;
+    constexpr uint32_t W = BSP_TREELET_BYTES / 4;
     for (size_t m = (size_t)blockIdx.x * 256u + threadIdx.x; m < slots; m += (size_t)gridDim.x * 256u) {
         auto node8 = [&](size_t q) -> uint2 {
             if (q == 0 || q > nnodes) return make_uint2(0u, 0u);
@@ -499,9 +544,9 @@ __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const 
             if ((n[0] & 3u) == 3u) return make_uint2(3u | ((48u * (n[0] >> 2)) << 2), rec_off + 48u * n[1]);
             return make_uint2(n[0] & 3u, __float_as_uint(planes[q - 1]));
         };
-        uint32_t* o = tl + 20 * m;
+        uint32_t* o = tl + W * m;
         if (m == 0) {
-            for (int k = 0; k < 20; k++) o[k] = 0u;
+            for (uint32_t k = 0; k < W; k++) o[k] = 0u;
             continue;
         }
         const float4 lo = box[2 * (m - 1)], hi = box[2 * (m - 1) + 1];
@@ -513,6 +558,29 @@ __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const 
             o[6 + 2 * k] = n[k].x;
             o[7 + 2 * k] = n[k].y;
         }
+        const float4 c0 = cert[2 * (m - 1)], c1 = cert[2 * (m - 1) + 1];
+        const double E2 = c0.x;
+        uint32_t hb[6] = {0u, 0u, 0u, 0u, 0u, 0u};
+        float F = INFINITY;
+        if (E2 > 0.0 && E2 < INFINITY) {
+            F = f_rd(1e-10 / E2 * (1.0 - 0x1p-40));
+            // centre c (nearest f16) and radius r (rounded up) with [lo, hi] inside [c - r, c + r]
+            const double s = 1.0 / E2, sl = 0x1p-50;
+            const float nl[3] = {c0.y, c0.z, c0.w}, nh[3] = {c1.y, c1.z, c1.w};
+            for (int k = 0; k < 3; k++) {
+                const double a = nl[k] * s, z = nh[k] * s;
+                const double lo = a - fabs(a) * sl, hi = z + fabs(z) * sl;
+                const uint32_t cb = __half_as_ushort(__float2half_rn((float)(0.5 * (lo + hi))));
+                const double c = (double)__half2float(__ushort_as_half((unsigned short)cb));
+                const double r = fmax(hi - c, c - lo);
+                hb[k] = cb;
+                hb[3 + k] = h_ru(f_ru(r * (1.0 + 0x1p-40)));
+            }
+        }
+        o[20] = __float_as_uint(F);
+        o[21] = hb[0] | (hb[1] << 16);
+        o[22] = hb[2] | (hb[3] << 16);
+        o[23] = hb[4] | (hb[5] << 16);
     }
 }
 
@@ -537,17 +605,18 @@ int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes
 {
     // content boxes: leaves, then each depth bottom-up (depth d holds nodes [2^d - 1, 2^(d+1) - 1))
     float4* box = reinterpret_cast<float4*>(box_scratch);
+    float4* cert = box + 2 * (size_t)nnodes;
     const uint32_t g0 = std::min<uint32_t>(16384, (nnodes + 255) / 256);
-    hipLaunchKernelGGL(k_leaf_boxes, dim3(g0), dim3(256), 0, s, tree, nnodes, pos, idx, ids, nids, box);
+    hipLaunchKernelGGL(k_leaf_boxes, dim3(g0), dim3(256), 0, s, tree, nnodes, pos, idx, ids, nids, box, cert);
     uint32_t depth = 0;
     while ((2ull << depth) - 1 < nnodes) depth++;   // the deepest level
     for (int d = (int)depth - 1; d >= 0; d--) {
         const uint32_t lo = (1u << d) - 1u, hi = std::min<uint32_t>(nnodes, (2u << d) - 1u);
         const uint32_t g = std::min<uint32_t>(16384, (hi - lo + 255) / 256);
-        hipLaunchKernelGGL(k_node_boxes, dim3(g), dim3(256), 0, s, tree, nnodes, lo, hi, box);
+        hipLaunchKernelGGL(k_node_boxes, dim3(g), dim3(256), 0, s, tree, nnodes, lo, hi, box, cert);
     }
     const uint32_t g1 = std::min<uint32_t>(16384, (nnodes + 256) / 256 + 1);
-    hipLaunchKernelGGL(k_bsp_repack, dim3(g1), dim3(256), 0, s, tree, planes, nnodes, rec_off, box, margin,
+    hipLaunchKernelGGL(k_bsp_repack, dim3(g1), dim3(256), 0, s, tree, planes, nnodes, rec_off, box, cert, margin,
                        reinterpret_cast<uint32_t*>(blob));
     if (nids) {
         const uint32_t g2 = std::min<uint32_t>(16384, (nids + 255) / 256 + 1);

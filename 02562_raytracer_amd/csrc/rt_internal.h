@@ -19,11 +19,12 @@ struct DevScene {
     const rt_material* mats;
     const uint32_t* lights;
     uint32_t nverts, ntris, nmats, nlights;
-    // BSP: one allocation [80-B treelets | 48-B records] (rt_api.cpp rt_upload_bsp):
-    // treelet of 1-based node M at 80*M holds M's content box (min.xyz, max.xyz: the
-    // triangles its subtree references, expanded) and nodes M, 2M, 2M+1, 4M..4M+3 (8 B
-    // each: interior {axis, plane bits}, leaf {3 | (48*count) << 2, first record's byte
-    // offset}); children implicit (2i+1, 2i+2 0-based, src/data_structures/bsp_tree.rs:137-140).
+    // BSP: one allocation [96-B treelets | 48-B records] (rt_api.cpp rt_upload_bsp):
+    // treelet of 1-based node M at 96*M holds M's content box (min.xyz, max.xyz: the
+    // triangles its subtree references), nodes M, 2M, 2M+1, 4M..4M+3 (8 B each:
+    // interior {axis, plane bits}, leaf {3 | (48*count) << 2, first record's byte
+    // offset}; children implicit, 2i+1, 2i+2 0-based, src/data_structures/bsp_tree.rs:137-140)
+    // and the certification data of its subtree (rt_bsp_build.hip k_bsp_repack).
     const uint2* bsp_nodes;       // start of the allocation
     const float4* bsp_recs;       // = bsp_nodes + bsp_rec_off: v0, e0=v1-v0, e1=v2-v0, n=cross(e0,e1)
     uint32_t bsp_bytes;           // size of the allocation (buffer-resource range)
@@ -38,11 +39,16 @@ struct DevScene {
     uint32_t bvh_rec_off;
     const uint32_t* bvh_ids;
     uint32_t bvh_nnodes;
-    // RT_OPT_BSP_CULL: the BSP walk skips a subtree whose content box the ray misses
-    // by more than this fraction of |tn| + |tf| (2^-18; +inf turns culling off
-    // without a branch on a uniform flag, rt_kernels.hip bsp_box_miss)
+    // RT_OPT_BSP_CULL: the BSP walk skips a subtree whose content box, grown by a
+    // margin, the ray misses by more than this fraction of |tn| + |tf| (2^-18; +inf
+    // turns culling off without a branch on a uniform flag, rt_kernels.hip bsp_box_miss)
     float bsp_cull_gap;
-    float bsp_margin;             // the content boxes' scene margin (rt_kernels.hip bsp_box_miss)
+    // the margin, as data for both culling modes (bsp_box_miss):
+    //   m = D1 * (cull_k1 * w1 / max(F, 2 Dlb - 20u w1) + cull_k3) + max(|o|inf * cull_ko, bsp_margin)
+    // certified (RT_BSP_CULL_CERTIFIED): k1 = 36u, k3 = 2u, ko = 2^-19, bsp_margin = 2^-19 x scene;
+    // fast (RT_BSP_CULL_FAST): k1 = k3 = 0, ko = 2^-10, bsp_margin = 2^-10 x scene
+    float bsp_margin;
+    float cull_k1, cull_k3, cull_ko;
 };
 
 // Work mapping + outputs of one launch.
@@ -123,9 +129,10 @@ struct BspDeviceOut {
 int build_bsp_device(const float4* pos, const uint4* idx, uint32_t ntris, uint32_t max_depth, uint32_t max_leaf,
                      int num_cus, hipStream_t stream, BspDeviceOut& out, rt_bsp_build_times* times, std::string& err);
 // traversal layout of a BSP from its reference-layout arrays (rt_upload_bsp's repack, on device):
-// 80-B treelets (content box + 7 nodes, BSP_TREELET_BYTES) then the 48-B records;
-// box_scratch: nnodes x 32 B of device memory for the content boxes
-constexpr uint32_t BSP_TREELET_BYTES = 80;
+// 96-B treelets (content box + 7 nodes + certification data, BSP_TREELET_BYTES)
+// then the 48-B records; box_scratch: nnodes x 64 B of device memory for the
+// content boxes and the certification data
+constexpr uint32_t BSP_TREELET_BYTES = 96;
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
                       const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,
                       void* box_scratch, hipStream_t stream);

@@ -17,7 +17,7 @@
 //     gives a refill's lanes the iterations of one pixel (coherent rays);
 //   * ray state machine with ONE traversal call site: each trip every tracing
 //     lane advances its ray (camera / bounce closest-hit, or a shadow any-hit)
-//     by one 80-B load: a treelet (its subtree's content box, tested first:
+//     by one 96-B load: a treelet (its subtree's content box, tested first:
 //     subtree culling, then three BSP levels walked), or a leaf's triangle
 //     records (two tests per trip); lanes whose ray ended wait and
 //     shade together once few lanes still trace (shading threshold, chosen
@@ -536,7 +536,7 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 // issues the same five 16-B loads at one base offset, before any decision
 // (one memory round trip per trip):
 //   * a lane inside a leaf tests its 48-B record (and the next one, below);
-//   * a lane walking nodes reads the 80-B treelet of its node m
+//   * a lane walking nodes reads the 96-B treelet of its node m
 //     (rt_bsp_build.hip k_bsp_repack: m's content box | nodes m | 2m, 2m+1 |
 //     4m..4m+3), tests the content box (bsp_walk) and walks up to three
 //     levels with no further load.
@@ -545,32 +545,29 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 // trip on); an empty leaf, or a leaf tested without a hit, pops.  Leaf ranges
 // (leaf_k, leaf_end, hit_k) are byte offsets of records in that buffer.
 // A second triangle test of a leaf in the same trip (BSP walk).  A leaf
-// lane's trip loads 80 B at its record: the 48-B record it tests and the
-// first 32 B of the next one (`nx`, `r1`; records of a leaf are 48 B apart).  The
-// next record is tested in order, after the first one's accept has narrowed
-// tmax, exactly as one test per trip would; its last 16 B cost one more
-// round trip (loading them with the trip's five loads, RT_LEAF_PRELOAD, was no
-// faster: profiles/r03/ab_pre_c*.txt).  A walk that stops at its first hit
-// (anyhit) stops here too.
+// lane's trip loads 96 B at its record (the treelet size): the 48-B record it
+// tests and the whole next one (`nx`, `r1`, `r2`; records of a leaf are 48 B
+// apart).  The next record is tested in order, after the first one's accept
+// has narrowed tmax, exactly as one test per trip would.  A walk that stops at
+// its first hit (anyhit) stops here too.
 // Two tests per trip take the per-trip costs (the check, the walking half of
 // the wave, the pop) off the leaf work: config 3 +2.9 %, config 4 +12 %,
 // config 5 (32-triangle leaves) +20 % (profiles/r02/ab_lt2.txt); three or more
 // per trip, or the same for the BVH walk (leaves of at most 4), were slower
-// (ab_lt.txt).
+// (ab_lt.txt).  (With 80-B treelets the second record's last 16 B took one
+// more round trip; loading them with the trip's loads was no faster then,
+// profiles/r03/ab_pre_c*.txt.  The 96-B treelets of the certified culling load
+// them anyway.)
 #ifndef RT_LEAF_TESTS
 #define RT_LEAF_TESTS 2   // triangle tests per leaf trip of the BSP walk: 1 or 2
-#endif
-#ifndef RT_LEAF_PRELOAD
-#define RT_LEAF_PRELOAD 0
 #endif
 template <bool COUNT, bool CULL, class LOG>
 __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const v4u r1, const v4u q5,
                                                const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
     if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
-        // the trip's 80-B load holds this record's first 32 B (nx, r1); its last
-        // 16 B come with the trip's loads too (RT_LEAF_PRELOAD) or one round trip later
-        const v4u r2 = RT_LEAF_PRELOAD ? q5 : __builtin_amdgcn_raw_buffer_load_b128(rs, t.leaf_k + 32u, 0, 0);
+        // the trip's 96-B load holds this whole record (nx, r1, r2 = q5)
+        const v4u r2 = q5;
         lg.tested(t.leaf_k);
         if (COUNT) {
             c.v[C_IDS]++;
@@ -628,16 +625,25 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // Subtree culling (RT_OPT_BSP_CULL, DESIGN.md section 4 "Subtree culling"): a
 // trip that starts at node M first tests the ray interval [tmin, tmax] against
 // M's content box -- the union of the bounding boxes of the triangles M's
-// leaves reference -- grown by a margin of 2^-10 of the larger of the scene's
-// and the ray origin's coordinate magnitude (dscene = 2^-10 x the scene's).  If
-// the interval misses it by a clear gap, no triangle of the subtree can be
-// accepted inside the interval, so the reference's walk of that subtree
-// (bsp.wgsl:10-81: every leaf tested without a hit, every pending entry pushed
-// inside it popped again) ends where the next pop starts: the walk pops at
-// once.  Which triangle is hit, and where, does not change; only hitless work
-// is skipped.  An axis whose direction component is below the shader's 1e-8
-// cut (inv is then +-1e8 or the NaN flag, see bsp_inv1) constrains nothing: the
-// NaN drops out of fminf / fmaxf.
+// leaves reference -- grown by a margin m.  If the interval misses it by a
+// clear gap, no triangle of the subtree can be accepted inside the interval,
+// so the reference's walk of that subtree (bsp.wgsl:10-81: every leaf tested
+// without a hit, every pending entry pushed inside it popped again) ends where
+// the next pop starts: the walk pops at once.  Which triangle is hit, and
+// where, does not change; only hitless work is skipped.
+// The margin (DESIGN.md section 4 "Certified culling"):
+//   m = D1 * (k1 * w1 / max(F, 2 Dlb - 20u w1) + k3) + max(|o|inf * ko, dscene)
+// with D1 >= |v0 - o|_1 for every point v0 of the box, w1 = |w|_1, F = 1e-10 /
+// E2 and 2 Dlb a lower bound of |w . n*| / E2 over the subtree's normals from
+// the treelet's normal box (q5: centre and radius of n* / E2).  Certified mode (k1 = 36u, k3 = 2u, ko and
+// dscene 2^-19 of the magnitudes): m bounds the L-inf distance from the box of
+// every point o + dist*w where intersect_triangle (w7e3.wgsl:286-332) can
+// accept one of the subtree's triangles -- its f32 rounding, including
+// |denom| >= 1e-10 at grazing angles -- so the cull is exact for every ray.
+// Fast mode (k1 = k3 = 0, ko and dscene 2^-10): the round-3 margin, not a bound.
+// An axis whose direction component is below the shader's 1e-8 cut (inv is
+// then +-1e8 or the NaN flag, see bsp_inv1) constrains nothing: the NaN drops
+// out of fminf / fmaxf.
 // RT_BSP_CULL 0 compiles the test out (A/B builds; RT_OPT_BSP_CULL then has no effect).
 #ifndef RT_BSP_CULL
 #define RT_BSP_CULL 1
@@ -652,25 +658,43 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // Off is data, not a branch on a uniform flag: a uniform bool kept as a lane
 // mask across the walk loops was reused under a wider exec mask by the
 // compiler (k_direct's shadow walk culled in the lanes that had been inactive
-// where the mask was computed; tests/test_gpu_cull.py caught it).
-__device__ __forceinline__ bool bsp_box_miss(const v4u q0, const v4u q1, const f3 o, const f3 inv, float tmin, float tmax,
-                                             float dscene, float gap, float& lo, float& hi)
+// where the mask was computed; tests/test_gpu_cull.py caught it).  The mode
+// is data for the same reason (DevScene cull_k1 / cull_k3 / cull_ko).
+__device__ __forceinline__ float h2f(uint32_t bits) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits); }
+__device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, const v4u q1, const v4u q5, const f3 o,
+                                             const f3 w, const f3 inv, float tmin, float tmax, float& lo, float& hi)
 {
-    const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
-    const float m = __builtin_fmaxf(mo * 0x1p-10f, dscene);
-    const float bmin[3] = {__uint_as_float(q0.x), __uint_as_float(q0.y), __uint_as_float(q0.z)};
-    const float bmax[3] = {__uint_as_float(q0.w), __uint_as_float(q1.x), __uint_as_float(q1.y)};
     const float oo[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
+    // vectors from the origin to the box's faces; D1 bounds |v0 - o|_1 over the box
+    float dl[3], dh[3], D1 = 0.0f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        dl[a] = __uint_as_float(a == 0 ? q0.x : (a == 1 ? q0.y : q0.z)) - oo[a];
+        dh[a] = __uint_as_float(a == 0 ? q0.w : (a == 1 ? q1.x : q1.y)) - oo[a];
+        D1 += __builtin_fmaxf(rt_absf(dl[a]), rt_absf(dh[a]));
+    }
+    const float w1 = rt_absf(w.x) + rt_absf(w.y) + rt_absf(w.z);
+    // |w . n*| / E2 >= 2 Dlb over the normal box, stored as centre c and
+    // radius r (f16): the box's minimum of |w . x| is |w . c| - |w| . r
+    // (fused multiply-adds of f16 and f32 operands: v_fma_mix_f32)
+    const float wc = __builtin_fmaf(w.z, h2f(q5.z & 0xFFFFu), __builtin_fmaf(w.y, h2f(q5.y >> 16), w.x * h2f(q5.y & 0xFFFFu)));
+    const float wr = __builtin_fmaf(rt_absf(w.z), h2f(q5.w >> 16),
+                                    __builtin_fmaf(rt_absf(w.y), h2f(q5.w & 0xFFFFu), rt_absf(w.x) * h2f(q5.z >> 16)));
+    const float dlb2 = rt_absf(wc) - wr;
+    const float den = __builtin_fmaxf(__uint_as_float(q5.x), dlb2 - (20.0f * 0x1p-24f) * w1);
+    const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
+    const float m = D1 * (S.cull_k1 * w1 * __builtin_amdgcn_rcpf(den) + S.cull_k3) +
+                    __builtin_fmaxf(mo * S.cull_ko, S.bsp_margin);
     float tn = tmin, tf = tmax;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : __builtin_nanf("");
-        const float t1 = (bmin[a] - m - oo[a]) * ib, t2 = (bmax[a] + m - oo[a]) * ib;
+        const float t1 = (dl[a] - m) * ib, t2 = (dh[a] + m) * ib;
         tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
         tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
     }
     // a clear gap: the rounding of the slab products cannot close it
-    const float e = (rt_absf(tn) + rt_absf(tf)) * gap;
+    const float e = (rt_absf(tn) + rt_absf(tf)) * S.bsp_cull_gap;
     // the interval the subtree's content can be hit in, widened by the same
     // tolerance (RT_BSP_CLIP; culling off: e = inf or NaN, lo = tmin, hi = tmax)
     lo = __builtin_fmaxf(tmin, tn - e);
@@ -679,22 +703,22 @@ __device__ __forceinline__ bool bsp_box_miss(const v4u q0, const v4u q1, const f
 }
 
 // The walking half of a BSP trip: node m (level 0), a child (level 1), a
-// grandchild (level 2) from the 80-B treelet in q0..q4 (rt_internal.h:
-// {box | box, node M | 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3}).  Returns true when
+// grandchild (level 2) from the 96-B treelet in q0..q5 (rt_internal.h:
+// {box | box, node M | 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3 | certification data}).  Returns true when
 // the walk reached a non-empty leaf (its range is set, its tests start next
 // trip); an empty leaf, or a subtree culled by its content box, sets pop.
 // (Testing the first record of a leaf in the trip that reaches it -- one more
 // round trip -- was slower: config 4 -3.7 %, config 5 -11 %, profiles/r02/ab_et1.txt.)
 template <bool COUNT>
 __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4u q0, const v4u q1, const v4u q2,
-                                         const v4u q3, const v4u q4, const f3 o, const f3 d, const f3 inv, Trav& t,
-                                         Counters& c, bool& pop)
+                                         const v4u q3, const v4u q4, const v4u q5, const f3 o, const f3 d, const f3 inv,
+                                         Trav& t, Counters& c, bool& pop)
 {
     uint32_t m = t.node;
     float lo = t.tmin, hi = t.tmax;   // the decisions' interval
     if (RT_BSP_CULL) {
         float blo, bhi;
-        if (bsp_box_miss(q0, q1, o, inv, t.tmin, t.tmax, S.bsp_margin, S.bsp_cull_gap, blo, bhi)) {
+        if (bsp_box_miss(S, q0, q1, q5, o, d, inv, t.tmin, t.tmax, blo, bhi)) {
             if (COUNT) c.v[C_CULLS]++;
             pop = true;
             return false;
@@ -738,8 +762,8 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
     const bool in_leaf = t.leaf_k != t.leaf_end;
-    // a leaf lane: its next 80 B of records (one whole, the next one's first
-    // 32 B); a walking lane: the 80-B treelet of its node
+    // a leaf lane: its next 96 B of records (two whole records); a walking
+    // lane: the 96-B treelet of its node
     const uint32_t base = in_leaf ? t.leaf_k : t.node * BSP_TREELET_BYTES;
     uint64_t tw = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
@@ -747,18 +771,10 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
     v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 48u, 0, 0);
     v4u q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 64u, 0, 0);
-    // RT_LEAF_PRELOAD: the second leaf test's last 16 B in the same round trip
-    // (1: every lane loads them, 2: leaf lanes only)
-    v4u q5 = {0u, 0u, 0u, 0u};
-    if (RT_LEAF_PRELOAD == 1 || (RT_LEAF_PRELOAD == 2 && in_leaf))
-        q5 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 80u, 0, 0);
+    v4u q5 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 80u, 0, 0);
     // keep the loads together (the compiler would sink the later ones
     // into the level-2 branch: a second round trip)
-#if RT_LEAF_PRELOAD
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5));
-#else
-    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4));
-#endif
     if (COUNT) {   // diagnostics: cycles from issuing the loads to their data
         tw = __builtin_amdgcn_s_memtime() - tw;
         if ((threadIdx.x & 63u) == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u))
@@ -766,7 +782,7 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     }
     bool done = false, pop = false;
     if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg);
-    else bsp_walk<COUNT>(S, stk, q0, q1, q2, q3, q4, o, d, inv, t, c, pop);
+    else bsp_walk<COUNT>(S, stk, q0, q1, q2, q3, q4, q5, o, d, inv, t, c, pop);
     if (pop) done = bsp_pop(stk, t);
     return done;
 }

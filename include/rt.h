@@ -173,10 +173,22 @@ typedef struct rt_ray_counts {
 /* option 8 is retired (trip-half postponement: slower on every BASELINE workload, and its
    per-trip test cost 1.7-4.4 % even when off, profiles/r02/sweep_KH_c5.txt, ab_nokh.txt) */
 #define RT_OPT_UNIT_ORDER      6  /* W7E3/W9E1 work-unit order: 0 chunk-major, 1 pixel-major (default) */
-#define RT_OPT_BSP_CULL        9  /* 1 (default): the BSP walk skips a subtree whose content box (the union of its
-                                     triangles' bounding boxes, grown by a margin) the ray interval misses -- the hit
-                                     is the same, the hitless work is skipped; 0: every node of bsp.wgsl's walk is
-                                     visited (the reference's tested-triangle sequence) */
+#define RT_OPT_BSP_CULL        9  /* subtree culling in the BSP walk: a subtree whose content
+                                     box (the union of its triangles' bounding boxes), grown by a margin, the ray
+                                     interval misses is skipped, and the walk's decisions use the interval clipped to
+                                     that box.  One of RT_BSP_CULL_*: */
+#define RT_BSP_CULL_OFF        0  /* every node of bsp.wgsl's walk is visited: the reference's walk and tested-
+                                     triangle sequence, by construction */
+#define RT_BSP_CULL_CERTIFIED  1  /* (default) the margin is a proven bound on how far an f32 accept of
+                                     intersect_triangle (w7e3.wgsl:286-332) can lie from its triangle's box, from the
+                                     subtree's largest edge and its box of normals: every hit (triangle, distance,
+                                     barycentrics) is bit-identical to RT_BSP_CULL_OFF for every ray; only hitless
+                                     work is skipped */
+#define RT_BSP_CULL_FAST       2  /* the margin is 2^-10 of the scene's / the ray origin's coordinate magnitude: not
+                                     a proven bound.  A ray within ~1e-5 rad of a large triangle's plane, where the
+                                     f32 test's hit point can sit off the triangle by more than the margin, can get
+                                     a different hit (measured: 2 of 400,000 deliberately grazing rays on a random
+                                     soup, none in any rendered frame) */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
 

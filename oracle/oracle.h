@@ -141,6 +141,10 @@ int or_render(const or_scene* s, const or_uniform* u, const float* jitter, int m
 int or_trace_one(const or_scene* s, int trav, int face_normals, const float o[3], const float d[3],
                  float tmin, float tmax, uint32_t* tri, float* dist);
 
+/* or_trace_one over n rays (8 floats each: origin, direction, tmin, tmax) on nthreads
+ * threads (closest hit: triangle id or 0xFFFFFFFF, distance) */
+int or_trace_many(const or_scene* s, int trav, uint32_t n, const float* rays, uint32_t* tri, float* dist, int nthreads);
+
 /* fs_main's camera ray (w7e3.wgsl:211-228 with uv of pixel (x, y), project.wgsl:131-148
  * jitter): origin and direction, as every render mode builds it. */
 void or_camera_ray(const or_uniform* u, uint32_t x, uint32_t y, float jx, float jy, float o[3], float d[3]);

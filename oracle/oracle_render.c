@@ -1563,6 +1563,38 @@ int or_trace_one(const or_scene* s, int trav, int face_normals, const float o[3]
     return hit;
 }
 
+/* or_trace_one over n rays (8 floats each: origin, direction, tmin, tmax) on
+ * nthreads threads: closest hit (triangle id or 0xFFFFFFFF, distance) */
+typedef struct {
+    const or_scene* s;
+    int trav;
+    uint32_t n, nth, k;
+    const float* rays;
+    uint32_t* tri;
+    float* dist;
+} ManyJob;
+static void* many_worker(void* p)
+{
+    ManyJob* J = (ManyJob*)p;
+    const uint32_t k = __atomic_fetch_add(&J->k, 1u, __ATOMIC_RELAXED);
+    for (uint32_t i = k; i < J->n; i += J->nth) {
+        const float* q = J->rays + 8 * (size_t)i;
+        or_trace_one(J->s, J->trav, 1, q, q + 3, q[6], q[7], J->tri + i, J->dist + i);
+    }
+    return NULL;
+}
+int or_trace_many(const or_scene* s, int trav, uint32_t n, const float* rays, uint32_t* tri, float* dist, int nthreads)
+{
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 256) nthreads = 256;
+    ManyJob J = {s, trav, n, (uint32_t)nthreads, 0u, rays, tri, dist};
+    pthread_t th[256];
+    for (int i = 1; i < nthreads; i++) pthread_create(&th[i], NULL, many_worker, &J);
+    many_worker(&J);
+    for (int i = 1; i < nthreads; i++) pthread_join(th[i], NULL);
+    return 0;
+}
+
 void or_camera_ray(const or_uniform* u, uint32_t x, uint32_t y, float jx, float jy, float o[3], float d[3])
 {
     Cam cam = make_cam(u);

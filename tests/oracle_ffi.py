@@ -311,6 +311,18 @@ def trace_one(scene, trav, o, d, tmin, tmax, face_normals=1):
     return bool(hit), tri.value, dist.value
 
 
+def trace_many(scene, trav, rays, nthreads=None):
+    """or_trace_many: closest hits of rays float32[n, 8] -> (tri uint32[n], dist float32[n])."""
+    rays = np.ascontiguousarray(rays, dtype=np.float32).reshape(-1, 8)
+    n = rays.shape[0]
+    tri = np.zeros(n, np.uint32)
+    dist = np.zeros(n, np.float32)
+    nt = nthreads or min(16, os.cpu_count() or 1)
+    lib().or_trace_many(C.byref(scene.s), TRAVS[trav], n, rays.ctypes.data_as(f32p), tri.ctypes.data_as(u32p),
+                        dist.ctypes.data_as(f32p), nt)
+    return tri, dist
+
+
 def camera_ray(uniform, x, y, jx=0.0, jy=0.0):
     """fs_main's camera ray for pixel (x, y): (origin, direction) float32[3]."""
     o = np.zeros(3, dtype=np.float32)

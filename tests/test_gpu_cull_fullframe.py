@@ -1,6 +1,7 @@
 """Subtree culling (RT_OPT_BSP_CULL, DESIGN.md section 4 "Subtree culling") on
-the BASELINE workloads at full size: every frame rendered with culling on (the
-default) equals the frame rendered with it off -- the reference's walk,
+the BASELINE workloads at full size: every frame rendered with culling on --
+certified (the default, exact by proof) and fast (the round-3 margin, exact by
+these measurements only) -- equals the frame rendered with it off -- the reference's walk,
 bsp.wgsl:10-81, which the rest of the suite pins to the oracle and the oracle
 to the reference's own JS walk -- bit for bit: every pixel's accumulated
 radiance (any single sample that differed would change its pixel's average),
@@ -45,16 +46,19 @@ def test_full_frame_cull_equals_reference_walk(rt, gpu, configs, config, spp):
         ctx.upload_bsp(mesh.bsp_tree())
         ctx.set_environment(wl.env)
         ctx.set_uniforms(rt.make_uniform(*wl.camera, wl.width, wl.height))
-        off = _frame(rt, ctx, wl, spp, 0)
-        on = _frame(rt, ctx, wl, spp, 1)
+        off = _frame(rt, ctx, wl, spp, rt._ffi.RT_BSP_CULL_OFF)
+        ons = [_frame(rt, ctx, wl, spp, m) for m in (rt._ffi.RT_BSP_CULL_CERTIFIED, rt._ffi.RT_BSP_CULL_FAST)]
     finally:
         ctx.close()
-    diff = int((off[0] != on[0]).any(axis=2).sum())
-    assert diff == 0, f"config {config}: {diff} pixels' radiance differs with culling"
-    assert np.array_equal(off[1], on[1]), "primary-hit ids differ with culling"
-    for k in ("samples", "primary", "shadow", "bounce"):
-        assert off[2][k] == on[2][k], (k, off[2][k], on[2][k])
-    assert off[2]["subtree_culls"] == 0 and on[2]["subtree_culls"] > 0
-    # the work culling saves (printed for the log; the bench reports it too)
-    print(f"config {config}: interior nodes {on[2]['node_interior'] / off[2]['node_interior']:.3f}, "
-          f"triangle tests {on[2]['tri_tests'] / off[2]['tri_tests']:.3f} of the unculled walk")
+    assert off[2]["subtree_culls"] == 0
+    for on, name in zip(ons, ("certified", "fast")):
+        diff = int((off[0] != on[0]).any(axis=2).sum())
+        assert diff == 0, f"config {config}: {diff} pixels' radiance differs with {name} culling"
+        assert np.array_equal(off[1], on[1]), f"primary-hit ids differ with {name} culling"
+        for k in ("samples", "primary", "shadow", "bounce"):
+            assert off[2][k] == on[2][k], (name, k, off[2][k], on[2][k])
+        # the work culling saves (printed for the log; the bench reports it too)
+        print(f"config {config} {name}: culls {on[2]['subtree_culls']}, interior nodes "
+              f"{on[2]['node_interior'] / off[2]['node_interior']:.3f}, "
+              f"triangle tests {on[2]['tri_tests'] / off[2]['tri_tests']:.3f} of the unculled walk")
+    assert ons[1][2]["subtree_culls"] > 0

@@ -70,9 +70,109 @@ void walk_sim_culls(double* out) { for (int i = 0; i < 32; i++) out[i] = g_cull[
 void walk_sim_root_only(int r) { g_root_only = r; }   /* nnodes x 6: content box (min.xyz, max.xyz) of each node's subtree, or NULL */
 void walk_sim_boxes(const float* b) { g_boxes = b; }
 static float g_tn, g_tf;   /* the ray interval clipped to the last tested box */
+/* WALK_CERT: the certified margin (DESIGN.md section 4 "Certified culling"):
+ * g_cert[node*7] = E2 (max over the subtree's triangles of max(|e0|inf, |e1|inf)^2),
+ * +1..3 / +4..6 = the box of n* / (2 E2) over them (lower / upper) */
+static const double* g_cert = 0;
+static double g_cert_mag = 0;
+static int g_cert_floor_only = 0;
+void walk_sim_cert(const double* c, double mag, int floor_only) { g_cert = c; g_cert_mag = mag; g_cert_floor_only = floor_only; }
+double g_cert_margin_sum = 0, g_cert_margin_n = 0;
+double walk_sim_cert_mean(void) { return g_cert_margin_n ? g_cert_margin_sum / g_cert_margin_n : 0; }
+static int g_cert_is_floor = 0;
+double g_lost[4];
+void walk_sim_lost(double* o) { for (int i = 0; i < 4; i++) o[i] = g_lost[i]; }
+static double cert_margin(uint32_t node, v3 o, v3 d, const float* b)
+{
+    const double u = 0x1p-24;
+    const double* c = g_cert + 7 * (size_t)node;
+    double E2 = c[0];
+    double w1 = fabs(d.x) + fabs(d.y) + fabs(d.z);
+    double d1 = 0;
+    for (int k = 0; k < 3; k++) {
+        double a = fabs(b[k] - comp(o, k)), e = fabs(b[3 + k] - comp(o, k));
+        d1 += a > e ? a : e;
+    }
+    double lo = 0, hi = 0;
+    for (int k = 0; k < 3; k++) {
+        double p = comp(d, k) * c[1 + k], q = comp(d, k) * c[4 + k];
+        lo += p < q ? p : q;
+        hi += p < q ? q : p;
+    }
+    double dlb = lo > 0 ? lo : (hi < 0 ? -hi : 0);
+    double den = 2 * dlb - 32 * u * w1;
+    double fl = 1e-10 / E2;
+    if (g_cert_floor_only || den < fl) den = fl;
+    if (g_cert_floor_only == 2) return 1e30;
+    g_cert_is_floor = den == fl;
+    double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));
+    return 34 * u * d1 * w1 / den + 2 * u * d1 + 0x1p-20 * (om + g_cert_mag);
+}
+/* WALK_CELLS: n x 6 doubles, the box of the cells of the subtree's non-empty
+ * leaves (the cells are the half-space intersections along the path: +-inf
+ * where unbounded) -- every accept of the reference walk in the subtree lies
+ * in one of them on every axis with |d| >= 1e-8 */
+static const double* g_cells = 0;
+void walk_sim_cells(const double* c) { g_cells = c; }
+static int cell_clip(uint32_t node, v3 o, v3 d, double* t0p, double* t1p)
+{
+    const double* b = g_cells + 6 * (size_t)node;
+    double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));
+    double m = 0x1p-20 * (om + g_cert_mag);
+    double t0 = *t0p, t1 = *t1p;
+    for (int k = 0; k < 3; k++) {
+        double dk = comp(d, k), ok = comp(o, k);
+        if (!(fabs(dk) >= 1e-8)) continue;
+        double a = (b[k] - m - ok) / dk, cc = (b[3 + k] + m - ok) / dk;
+        if (a > cc) { double x = a; a = cc; cc = x; }
+        if (a > t0) t0 = a;
+        if (cc < t1) t1 = cc;
+    }
+    *t0p = t0;
+    *t1p = t1;
+    return t0 > t1 + (fabs(t0) + fabs(t1)) * 0x1p-18;
+}
 static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
 {
     const float* b = g_boxes + 6 * (size_t)node;
+    if (g_cells && b[0] <= b[3]) {
+        double c0 = tmin, c1 = tmax;
+        if (cell_clip(node, o, d, &c0, &c1)) return 1;
+        tmin = (float)c0 > tmin ? (float)c0 : tmin;   /* approximately: the model only counts trips */
+        tmax = (float)c1 < tmax ? (float)c1 : tmax;
+    }
+    if (g_cert && b[0] <= b[3]) {
+        double m = cert_margin(node, o, d, b);
+        g_cert_margin_sum += m; g_cert_margin_n += 1;
+        double t0 = tmin, t1 = tmax;
+        for (int k = 0; k < 3; k++) {
+            double dk = comp(d, k), ok = comp(o, k);
+            if (fabs(dk) < 1e-8) { if (ok < b[k] - m || ok > b[3 + k] + m) return 1; continue; }
+            double a = (b[k] - m - ok) / dk, cc = (b[3 + k] + m - ok) / dk;
+            if (a > cc) { double x = a; a = cc; cc = x; }
+            if (a > t0) t0 = a;
+            if (cc < t1) t1 = cc;
+        }
+        g_tn = (float)t0;
+        g_tf = (float)t1;
+        int miss = t0 > t1 + (fabs(t0) + fabs(t1)) * 0x1p-18;
+        if (!miss) {
+            /* would the fast margin (2^-10 of max(|o|, scene)) have culled? */
+            double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));
+            double mf = fmax(om, g_cert_mag) * 0x1p-10;
+            double a0 = tmin, a1 = tmax;
+            for (int k = 0; k < 3; k++) {
+                double dk = comp(d, k), ok = comp(o, k);
+                if (fabs(dk) < 1e-8) continue;
+                double a = (b[k] - mf - ok) / dk, cc = (b[3 + k] + mf - ok) / dk;
+                if (a > cc) { double x = a; a = cc; cc = x; }
+                if (a > a0) a0 = a;
+                if (cc < a1) a1 = cc;
+            }
+            if (a0 > a1) g_lost[g_cert_is_floor] += 1;
+        }
+        return miss;
+    }
     g_tn = tmin;
     g_tf = tmax;
     if (b[0] > b[3]) return 1;   /* empty subtree */

@@ -101,26 +101,96 @@ def main():
         tb_lo = np.minimum(np.minimum(P3[idx[:, 0]], P3[idx[:, 1]]), P3[idx[:, 2]])
         tb_hi = np.maximum(np.maximum(P3[idx[:, 0]], P3[idx[:, 1]]), P3[idx[:, 2]])
         leaf = (tree[:, 0] & 3) == 3
-        for i in np.nonzero(leaf)[0]:
-            c, f = tree[i, 0] >> 2, tree[i, 1]
-            if c:
-                t = ids[f:f + c]
-                boxes[i, :3] = tb_lo[t].min(axis=0)
-                boxes[i, 3:] = tb_hi[t].max(axis=0)
-        for i in range(n - 1, -1, -1):
-            if not leaf[i] and 2 * i + 2 < n:
-                boxes[i, :3] = np.minimum(boxes[2 * i + 1, :3], boxes[2 * i + 2, :3])
-                boxes[i, 3:] = np.maximum(boxes[2 * i + 1, 3:], boxes[2 * i + 2, 3:])
+        cnt = tree[:, 0] >> 2
+        lv = np.nonzero(leaf & (cnt > 0))[0]
+        first = tree[lv, 1].astype(np.int64)
+
+        def leaf_reduce(vals, red):
+            # per non-empty leaf: red over its triangles' vals (leaf ranges are contiguous in ids order)
+            order = np.argsort(first, kind="stable")
+            st = first[order]
+            v = vals[ids]
+            out = np.empty((len(lv),) + vals.shape[1:], vals.dtype)
+            out[order] = red.reduceat(v, st, axis=0)
+            return out
+
+        def up(arr, red):
+            # bottom-up union over interior nodes, one depth level at a time
+            dmax = int(np.floor(np.log2(n + 1)))
+            for dd in range(dmax, -1, -1):
+                a, b = 2 ** dd - 1, min(2 ** (dd + 1) - 1, n)
+                i = np.arange(a, b)
+                i = i[(~leaf[i]) & (2 * i + 2 < n)]
+                arr[i] = red(arr[2 * i + 1], arr[2 * i + 2])
+
+        boxes[lv, :3] = leaf_reduce(tb_lo, np.minimum)
+        boxes[lv, 3:] = leaf_reduce(tb_hi, np.maximum)
+        up(boxes, lambda x, y: np.concatenate([np.minimum(x[:, :3], y[:, :3]), np.maximum(x[:, 3:], y[:, 3:])], 1))
         # conservative expansion: 2^-k of the scene's coordinate magnitude (WALK_MARGIN_LG, default 14)
         scale = float(np.abs(pos[:, :3]).max())
         mg = np.float32(scale * 2.0 ** -float(os.environ.get("WALK_MARGIN_LG", "14")))
         boxes[:, :3] -= mg
         boxes[:, 3:] += mg
         boxes = np.ascontiguousarray(boxes)
+        if os.environ.get("WALK_CERT"):
+            # raw content boxes (the certified margin is applied per ray) and the
+            # per-subtree certification data: E2 and the box of n*/(2 E2)
+            boxes[:, :3] += mg
+            boxes[:, 3:] -= mg
+            V32 = pos[:, :3].astype(np.float32)
+            v0, v1, v2 = V32[idx[:, 0]], V32[idx[:, 1]], V32[idx[:, 2]]
+            e0 = (v1 - v0).astype(np.float32).astype(np.float64)
+            e1 = (v2 - v0).astype(np.float32).astype(np.float64)
+            nst = np.cross(e0, e1)
+            Et2 = np.maximum(np.abs(e0).max(1), np.abs(e1).max(1)) ** 2
+            cert = np.zeros((n, 7))
+            e2 = np.zeros(n)
+            e2[lv] = leaf_reduce(Et2, np.maximum)
+            up(e2, np.maximum)
+            cert[:, 0] = e2
+            lo_raw = np.full((n, 3), np.inf)
+            hi_raw = np.full((n, 3), -np.inf)
+            lo_raw[lv] = leaf_reduce(nst, np.minimum)
+            hi_raw[lv] = leaf_reduce(nst, np.maximum)
+            up(lo_raw, np.minimum)
+            up(hi_raw, np.maximum)
+            ok = cert[:, 0] > 0
+            cert[ok, 1:4] = lo_raw[ok] / (2 * cert[ok, 0, None])
+            cert[ok, 4:7] = hi_raw[ok] / (2 * cert[ok, 0, None])
+            cert[~ok, 0] = 1.0
+            cert = np.ascontiguousarray(cert)
+            if os.environ.get("WALK_CELLS"):
+                cells = np.empty((n, 6))
+                cells[0, :3] = -np.inf
+                cells[0, 3:] = np.inf
+                for dd in range(0, int(np.floor(np.log2(n + 1)))):
+                    a, b = 2 ** dd - 1, min(2 ** (dd + 1) - 1, n)
+                    i = np.arange(a, b)
+                    i = i[(~leaf[i]) & (2 * i + 2 < n)]
+                    ax = (tree[i, 0] & 3).astype(np.int64)
+                    pl = planes[i].astype(np.float64)
+                    L_, R_ = 2 * i + 1, 2 * i + 2
+                    cells[L_] = cells[i]
+                    cells[R_] = cells[i]
+                    cells[L_, 3 + ax] = pl
+                    cells[R_, ax] = pl
+                occ = np.empty((n, 6))
+                occ[:, :3] = np.inf
+                occ[:, 3:] = -np.inf
+                occ[lv] = cells[lv]
+                up(occ, lambda x, y: np.concatenate([np.minimum(x[:, :3], y[:, :3]), np.maximum(x[:, 3:], y[:, 3:])], 1))
+                occ = np.ascontiguousarray(occ)
+                print("occupied-cell boxes: unbounded sides at the root", int(np.isinf(occ[0]).sum()))
+            boxes = np.ascontiguousarray(boxes)
     L = lib()
     P = ctypes.c_void_p
     L.walk_sim_levels(int(os.environ.get("WALK_LEVELS", "3")))
     L.walk_sim_boxes(P(boxes.ctypes.data) if boxes is not None else None)
+    if boxes is not None and os.environ.get("WALK_CERT"):
+        L.walk_sim_cert.argtypes = [ctypes.c_void_p, ctypes.c_double, ctypes.c_int]
+        L.walk_sim_cert(cert.ctypes.data, float(np.abs(pos[:, :3]).max()), int(os.environ.get("WALK_CERT_FLOOR", "0")))
+        if os.environ.get("WALK_CELLS"):
+            L.walk_sim_cells(P(occ.ctypes.data))
     L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
     L.walk_sim_cull_every(int(os.environ.get("WALK_CULL_EVERY", "0")))
     L.walk_sim_clip(int(os.environ.get("WALK_CLIP", "0")))
@@ -156,6 +226,12 @@ def main():
         L.walk_sim_culls(P(cu.ctypes.data))
         print("culls per ray by depth:", {d: round(v / len(R), 3) for d, v in enumerate(cu[:32]) if v},
               "of which at leaves:", round(cu[32] / len(R), 3))
+    if boxes is not None and os.environ.get("WALK_CERT"):
+        L.walk_sim_cert_mean.restype = ctypes.c_double
+        print("mean certified margin", L.walk_sim_cert_mean())
+        lo_ = np.zeros(4)
+        L.walk_sim_lost(P(lo_.ctypes.data))
+        print("fast culls lost by the certified test per ray: cone regime %.3f, floor regime %.3f" % (lo_[0] / len(R), lo_[1] / len(R)))
     print(f"config {cfgn}: {len(R)} rays ({sum(flags)} any-hit), {time.time() - t0:.1f} s")
     for v in range(5 if boxes is not None else 3):
         s = {k: round(out[v, i] / len(R), 3) for i, k in enumerate(NAMES)}
