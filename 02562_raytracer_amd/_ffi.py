@@ -34,6 +34,7 @@ RT_OPT_UNIT_ORDER = 6
 RT_OPT_BSP_CULL = 9
 RT_BSP_CULL_OFF, RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_FAST = range(3)
 RT_OPT_KERNEL_TIMING = 7
+RT_COMM_ID_BYTES = 128
 
 MODES = {"W1E6": RT_MODE_W1E6, "W6E1": RT_MODE_W6E1, "PROJECT": RT_MODE_PROJECT, "W7E3": RT_MODE_W7E3,
          "W9E1": RT_MODE_W9E1, "W8E1": RT_MODE_W8E1, "W8E2": RT_MODE_W8E2, "W8E3": RT_MODE_W8E3,
@@ -156,6 +157,10 @@ SIGNATURES = {
                                   C.POINTER(RayCounts)]),
     "rt_tileset_local_tiles": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
     "rt_unpack_tiles": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.c_uint32, vp, vp, vp, vp]),
+    "rt_comm_unique_id": (C.c_int, [vp]),
+    "rt_comm_init": (C.c_int, [vp, C.c_uint32, C.c_uint32, vp]),
+    "rt_comm_destroy": (C.c_int, [vp]),
+    "rt_gather_tiles": (C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp]),
     "rt_trace_rays": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp]),
     "rt_last_counts": (C.c_int, [vp, C.POINTER(RayCounts)]),
     "rt_selftest_math": (C.c_int, [vp, C.c_uint32, C.c_float, C.c_float, u32p]),

@@ -387,6 +387,28 @@ class Context:
         self._chk(F.lib().rt_unpack_tiles(self._h, width, height, nranks, vpn(packed_accum), vpn(packed_ids),
                                           vpn(frame_accum), vpn(frame_ids)))
 
+    # ---- the tile gather over RCCL (include/rt.h "multi-GPU")
+    @staticmethod
+    def comm_unique_id():
+        """rt_comm_unique_id: a new communicator id (bytes, RT_COMM_ID_BYTES)."""
+        buf = (C.c_uint8 * F.RT_COMM_ID_BYTES)()
+        F.check(F.lib().rt_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        """rt_comm_init: join communicator `uid` as `rank` of `nranks` (collective)."""
+        buf = (C.c_uint8 * F.RT_COMM_ID_BYTES).from_buffer_copy(uid)
+        self._chk(F.lib().rt_comm_init(self._h, nranks, rank, buf))
+
+    def comm_destroy(self):
+        self._chk(F.lib().rt_comm_destroy(self._h))
+
+    def gather_tiles(self, width, height, local_accum, local_ids, frame_accum=None, frame_ids=None):
+        """rt_gather_tiles: every rank's packed tiles to rank 0's frame (device pointers)."""
+        vpn = (lambda p: C.c_void_p(p) if p else None)
+        self._chk(F.lib().rt_gather_tiles(self._h, width, height, vpn(local_accum), vpn(local_ids), vpn(frame_accum),
+                                          vpn(frame_ids)))
+
     def trace_rays(self, trav, rays, anyhit=None):
         """rt_trace_rays on host arrays: rays float32[n, 8] (origin, direction,
         tmin, tmax), anyhit bool[n] or None.  Returns a structured array with the

@@ -2,7 +2,9 @@
 // wrapper (replaces src/gpu_handles.rs), storage-buffer uploads (replaces
 // src/bindings/*.rs create_buffer_init) with the MI355X data layout repack,
 // and RenderState::render (src/render_state.rs:483-561).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -10,6 +12,7 @@
 #include <cmath>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "host_types.h"
@@ -38,6 +41,10 @@ struct DevBuf {
         }
         n = bytes;
         return hipSuccess;
+    }
+    hipError_t ensure(size_t bytes)   // at least `bytes`, keeping a large enough block
+    {
+        return p && n >= bytes ? hipSuccess : alloc(bytes);
     }
     void adopt(void* q, size_t bytes)   // take ownership of a hipMalloc'ed block
     {
@@ -104,6 +111,10 @@ struct rt_ctx {
     bool ktiming = false;
     std::vector<hipEvent_t> kev;
     size_t kused = 0;   // events recorded since the last reset (2 per launch)
+    // rt_comm_init: the tile gather's RCCL communicator (rt_gather_tiles)
+    ncclComm_t comm = nullptr;
+    uint32_t comm_nranks = 0, comm_rank = 0;
+    DevBuf gather_accum, gather_ids;   // rank 0: every rank's packed tiles, rank-major
 };
 
 namespace {
@@ -226,6 +237,7 @@ void rt_destroy(rt_ctx* c)
     if (!c) return;
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
+    (void)rt_comm_destroy(c);
     for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -1029,6 +1041,146 @@ int rt_unpack_tiles(rt_ctx* c, uint32_t width, uint32_t height, uint32_t nranks,
     int r = rtk::launch_unpack(width, height, nranks, lt, reinterpret_cast<const float4*>(packed_accum), packed_ids,
                                reinterpret_cast<float4*>(frame_accum), frame_ids, c->stream);
     if (r) return fail(c, r, "rt_unpack_tiles: launch failed");
+    return RT_OK;
+}
+
+// ---- the tile gather over RCCL (rt.h "multi-GPU") ----------------------------
+// RCCL is resolved at run time (dlopen of librccl.so.1): the library loads on
+// hosts without it, and a process that already holds RCCL (PyTorch's) shares it.
+extern "C++" {
+namespace {
+struct Rccl {
+    void* h = nullptr;
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+    std::string err;
+};
+const Rccl& rccl()
+{
+    static Rccl r = [] {
+        Rccl x;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"}) {
+            x.h = dlopen(name, RTLD_NOW | RTLD_LOCAL);
+            if (x.h) break;
+        }
+        if (!x.h) {
+            const char* e = dlerror();
+            x.err = std::string("RCCL not found (librccl.so.1): ") + (e ? e : "");
+            return x;
+        }
+        auto sym = [&](auto& f, const char* n) { f = reinterpret_cast<std::remove_reference_t<decltype(f)>>(dlsym(x.h, n)); };
+        sym(x.get_unique_id, "ncclGetUniqueId");
+        sym(x.comm_init_rank, "ncclCommInitRank");
+        sym(x.comm_destroy, "ncclCommDestroy");
+        sym(x.send, "ncclSend");
+        sym(x.recv, "ncclRecv");
+        sym(x.group_start, "ncclGroupStart");
+        sym(x.group_end, "ncclGroupEnd");
+        sym(x.error_string, "ncclGetErrorString");
+        if (!x.get_unique_id || !x.comm_init_rank || !x.comm_destroy || !x.send || !x.recv || !x.group_start ||
+            !x.group_end || !x.error_string)
+            x.err = "RCCL lacks a symbol rt_comm needs";
+        return x;
+    }();
+    return r;
+}
+std::string nccl_msg(const Rccl& R, ncclResult_t e) { return R.error_string ? R.error_string(e) : "RCCL error"; }
+}  // namespace
+}
+
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES])
+{
+    static_assert(sizeof(ncclUniqueId) == RT_COMM_ID_BYTES, "RT_COMM_ID_BYTES");
+    if (!id) return RT_E_INVALID;
+    const Rccl& R = rccl();
+    if (!R.err.empty()) return fail(nullptr, RT_E_UNSUPPORTED, "rt_comm_unique_id: " + R.err);
+    ncclUniqueId u;
+    if (ncclResult_t e = R.get_unique_id(&u)) return fail(nullptr, RT_E_DEVICE, "ncclGetUniqueId: " + nccl_msg(R, e));
+    memcpy(id, &u, sizeof u);
+    return RT_OK;
+}
+
+int rt_comm_init(rt_ctx* c, uint32_t nranks, uint32_t rank, const uint8_t id[RT_COMM_ID_BYTES])
+{
+    if (!c || !id || nranks == 0 || rank >= nranks || nranks > 4096) return RT_E_INVALID;
+    if (c->comm) return fail(c, RT_E_INVALID, "rt_comm_init: the context already has a communicator");
+    const Rccl& R = rccl();
+    if (!R.err.empty()) return fail(c, RT_E_UNSUPPORTED, "rt_comm_init: " + R.err);
+    if (int r = set_dev(c)) return r;
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    ncclComm_t comm = nullptr;
+    if (ncclResult_t e = R.comm_init_rank(&comm, (int)nranks, u, (int)rank))
+        return fail(c, RT_E_DEVICE, "ncclCommInitRank: " + nccl_msg(R, e));
+    c->comm = comm;
+    c->comm_nranks = nranks;
+    c->comm_rank = rank;
+    return RT_OK;
+}
+
+int rt_comm_destroy(rt_ctx* c)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->comm) return RT_OK;
+    const Rccl& R = rccl();
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    ncclResult_t e = R.comm_destroy(c->comm);
+    c->comm = nullptr;
+    c->comm_nranks = c->comm_rank = 0;
+    c->gather_accum.reset();
+    c->gather_ids.reset();
+    if (e) return fail(c, RT_E_DEVICE, "ncclCommDestroy: " + nccl_msg(R, e));
+    return RT_OK;
+}
+
+int rt_gather_tiles(rt_ctx* c, uint32_t width, uint32_t height, const float* local_accum, const uint32_t* local_ids,
+                    float* frame_accum, uint32_t* frame_ids)
+{
+    if (!c || !local_accum || width == 0 || height == 0) return RT_E_INVALID;
+    if (!c->comm) return fail(c, RT_E_NOT_READY, "rt_gather_tiles: no communicator (rt_comm_init)");
+    const uint32_t N = c->comm_nranks, me = c->comm_rank;
+    const bool root = me == 0;
+    if (root && !frame_accum) return fail(c, RT_E_INVALID, "rt_gather_tiles: rank 0 needs frame_accum");
+    if (root && local_ids && !frame_ids) return fail(c, RT_E_INVALID, "rt_gather_tiles: rank 0 needs frame_ids");
+    if (int r = set_dev(c)) return r;
+    const Rccl& R = rccl();
+    const size_t px = (size_t)rt_tileset_local_tiles(width, height, N) * 64u;
+    if (!root) {
+        // one group: this rank's accumulation and ids to rank 0
+        ncclResult_t e = R.group_start();
+        if (!e) e = R.send(local_accum, px * 4, ncclFloat32, 0, c->comm, c->stream);
+        if (!e && local_ids) e = R.send(local_ids, px, ncclUint32, 0, c->comm, c->stream);
+        const ncclResult_t e2 = R.group_end();
+        if (e || e2) return fail(c, RT_E_DEVICE, "rt_gather_tiles send: " + nccl_msg(R, e ? e : e2));
+        return RT_OK;
+    }
+    // rank 0: every peer's packed tiles, rank-major beside its own (slot 0), in one group
+    HIPCHK(c, c->gather_accum.ensure(px * 16 * N));
+    if (local_ids) HIPCHK(c, c->gather_ids.ensure(px * 4 * N));
+    float* ga = c->gather_accum.as<float>();
+    uint32_t* gi = c->gather_ids.as<uint32_t>();
+    HIPCHK(c, hipMemcpyAsync(ga, local_accum, px * 16, hipMemcpyDeviceToDevice, c->stream));
+    if (local_ids) HIPCHK(c, hipMemcpyAsync(gi, local_ids, px * 4, hipMemcpyDeviceToDevice, c->stream));
+    if (N > 1) {
+        ncclResult_t e = R.group_start();
+        for (uint32_t p = 1; p < N && !e; p++) {
+            e = R.recv(ga + p * px * 4, px * 4, ncclFloat32, (int)p, c->comm, c->stream);
+            if (!e && local_ids) e = R.recv(gi + p * px, px, ncclUint32, (int)p, c->comm, c->stream);
+        }
+        const ncclResult_t e2 = R.group_end();
+        if (e || e2) return fail(c, RT_E_DEVICE, "rt_gather_tiles recv: " + nccl_msg(R, e ? e : e2));
+    }
+    int r = rtk::launch_unpack(width, height, N, (uint32_t)(px / 64), reinterpret_cast<const float4*>(ga),
+                               local_ids ? gi : nullptr, reinterpret_cast<float4*>(frame_accum),
+                               local_ids ? frame_ids : nullptr, c->stream);
+    if (r) return fail(c, r, "rt_gather_tiles: unpack launch failed");
     return RT_OK;
 }
 

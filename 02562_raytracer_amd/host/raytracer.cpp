@@ -311,7 +311,34 @@ void RenderState::release()
 {
     if (accum_) rt_device_free(gpu_.ctx(), accum_);
     if (ids_) rt_device_free(gpu_.ctx(), ids_);
-    accum_ = ids_ = nullptr;
+    if (tile_accum_) rt_device_free(gpu_.ctx(), tile_accum_);
+    if (tile_ids_) rt_device_free(gpu_.ctx(), tile_ids_);
+    accum_ = ids_ = tile_accum_ = tile_ids_ = nullptr;
+}
+
+void RenderState::set_tiling(uint32_t nranks, uint32_t rank, const uint8_t comm_id[RT_COMM_ID_BYTES])
+{
+    if (tiled_) throw Error(RT_E_INVALID, "set_tiling: already tiled");
+    gpu_.check(rt_comm_init(gpu_.ctx(), nranks, rank, comm_id), "communicator");
+    nranks_ = nranks;
+    rank_ = rank;
+    tiled_ = true;
+    alloc_tiles();
+}
+
+// the packed tile buffers of this rank for the current resolution (zeroed: the
+// accumulation of iteration 0 is not read)
+void RenderState::alloc_tiles()
+{
+    if (!tiled_) return;
+    rt_ctx* c = gpu_.ctx();
+    if (tile_accum_) rt_device_free(c, tile_accum_);
+    if (tile_ids_) rt_device_free(c, tile_ids_);
+    tile_accum_ = tile_ids_ = nullptr;
+    const size_t px = (size_t)rt_tileset_local_tiles(width_, height_, nranks_) * 64u;
+    gpu_.check(rt_device_alloc(c, px * 16, &tile_accum_), "tile accumulation buffer");
+    gpu_.check(rt_device_alloc(c, px * 4, &tile_ids_), "tile id buffer");
+    gpu_.check(rt_memset_device(c, tile_accum_, 0, px * 16), "clear tile accumulation");
 }
 
 void RenderState::setup_rendering(const SceneDescriptor& scene)
@@ -363,6 +390,7 @@ void RenderState::setup_rendering(const SceneDescriptor& scene)
     gpu_.check(rt_device_alloc(c, npx * 16, &accum_), "accumulation buffer");
     gpu_.check(rt_device_alloc(c, npx * 4, &ids_), "id buffer");
     gpu_.check(rt_memset_device(c, accum_, 0, npx * 16), "clear accumulation");
+    alloc_tiles();
     iteration_ = 0;
     update();
 }
@@ -384,10 +412,23 @@ void RenderState::update()
 
 void RenderState::render(uint32_t spp)
 {
-    const rt_tile region{0, 0, width_, height_};
-    gpu_.check(rt_render(gpu_.ctx(), mode_, trav_, &region, iteration_, spp, static_cast<float*>(accum_),
-                         static_cast<uint32_t*>(ids_), nullptr),
-               "render");
+    if (tiled_) {
+        // this rank's tiles, then every rank's tiles into rank 0's frame
+        const rt_tileset ts{rank_, nranks_};
+        gpu_.check(rt_render_tiles(gpu_.ctx(), mode_, trav_, &ts, iteration_, spp, static_cast<float*>(tile_accum_),
+                                   static_cast<uint32_t*>(tile_ids_), nullptr),
+                   "render tiles");
+        const bool root = rank_ == 0;
+        gpu_.check(rt_gather_tiles(gpu_.ctx(), width_, height_, static_cast<const float*>(tile_accum_),
+                                   static_cast<const uint32_t*>(tile_ids_), root ? static_cast<float*>(accum_) : nullptr,
+                                   root ? static_cast<uint32_t*>(ids_) : nullptr),
+                   "gather tiles");
+    } else {
+        const rt_tile region{0, 0, width_, height_};
+        gpu_.check(rt_render(gpu_.ctx(), mode_, trav_, &region, iteration_, spp, static_cast<float*>(accum_),
+                             static_cast<uint32_t*>(ids_), nullptr),
+                   "render");
+    }
     const bool path = mode_ == RT_MODE_W7E3 || mode_ == RT_MODE_W9E1 || mode_ == RT_MODE_W8E1 ||
                       mode_ == RT_MODE_W8E2 || mode_ == RT_MODE_W8E3 || mode_ == RT_MODE_W9E2 ||
                       mode_ == RT_MODE_W7E1 || mode_ == RT_MODE_W7E2 || mode_ == RT_MODE_W9E3;

@@ -7,6 +7,11 @@
 //   rt_render --scene NAME [--res WxH] [--spp N | --samples N] [--keys K1,K2 --updates N]
 //             [--selection K] [--subdiv K] [--camera-constant C] [--device-build]
 //             [--env-rgba FILE --env-size WxH] [--models DIR] [--out PREFIX]
+//   rt_render ... --nranks N --rank R --comm-file PATH [--device D]
+//                                        (one process per GPU: rank R renders its
+//                                        interleaved tiles, rank 0 gathers the frame
+//                                        over RCCL and writes it; rank 0 publishes the
+//                                        communicator id in PATH; device defaults to R)
 //   rt_render --camera-test K1,K2 N      (CPU: eye after N controller updates)
 //   rt_render --jitter SUBDIV HEIGHT     (CPU: the jitter table)
 //
@@ -14,10 +19,12 @@
 // PREFIX.rgba8 (the sRGB frame); one JSON summary line goes to stdout.
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
 #include <fstream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "raytracer.hpp"
@@ -87,6 +94,24 @@ static void write_file(const std::string& path, const void* p, size_t n)
     if (!f) throw Error(RT_E_INVALID, "cannot write " + path);
 }
 
+// the communicator id through a file: rank 0 writes it (then renames, so a
+// reader never sees a partial file), the other ranks wait for it
+static void publish_comm_id(const std::string& path, uint8_t id[RT_COMM_ID_BYTES], uint32_t rank)
+{
+    if (rank == 0) {
+        if (int r = rt_comm_unique_id(id)) throw Error(r, rt_last_error(nullptr));
+        write_file(path + ".tmp", id, RT_COMM_ID_BYTES);
+        if (std::rename((path + ".tmp").c_str(), path.c_str()) != 0) throw Error(RT_E_INVALID, "cannot publish " + path);
+        return;
+    }
+    for (int i = 0; i < 1200; i++) {   // up to 2 minutes
+        std::ifstream f(path, std::ios::binary);
+        if (f && f.read(reinterpret_cast<char*>(id), RT_COMM_ID_BYTES)) return;
+        std::this_thread::sleep_for(std::chrono::milliseconds(100));
+    }
+    throw Error(RT_E_NOT_READY, "no communicator id in " + path);
+}
+
 static std::string default_models_dir(const char* argv0)
 {
     // <repo>/02562_raytracer_amd/bin/rt_render -> <repo>/assets/models
@@ -152,8 +177,17 @@ int main(int argc, char** argv)
             opt.resolution = std::make_pair(w, h);
         }
         opt.device_build = flag("--device-build");
-        GpuHandles gpu(0);
+        const uint32_t nranks = arg("--nranks") ? (uint32_t)std::atoi(arg("--nranks")->c_str()) : 1;
+        const uint32_t rank = arg("--rank") ? (uint32_t)std::atoi(arg("--rank")->c_str()) : 0;
+        if (nranks == 0 || rank >= nranks) throw Error(RT_E_INVALID, "--rank must be below --nranks");
+        if (nranks > 1 && !arg("--comm-file")) throw Error(RT_E_INVALID, "--nranks needs --comm-file PATH");
+        GpuHandles gpu(arg("--device") ? std::atoi(arg("--device")->c_str()) : (int)rank);
         RenderState rs(gpu, find_scene(*name), opt);
+        if (const std::string* cf = arg("--comm-file")) {
+            uint8_t id[RT_COMM_ID_BYTES];
+            publish_comm_id(*cf, id, rank);
+            rs.set_tiling(nranks, rank, id);
+        }
         std::vector<uint8_t> env;
         if (const std::string* ef = arg("--env-rgba")) {
             unsigned w = 0, h = 0;
@@ -185,6 +219,7 @@ int main(int argc, char** argv)
             frames = 1;
         }
         const rt_ray_counts c = rs.last_counts();
+        if (rank != 0) return 0;   // the frame is rank 0's
         if (const std::string* out = arg("--out")) {
             const auto f = rs.frame();
             const auto ids = rs.hit_ids();

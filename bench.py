@@ -260,7 +260,15 @@ def main():
     acc_local = torch.empty((lt * 64, 4), dtype=torch.float32, device=dev)
     ids_local = torch.empty((lt * 64,), dtype=torch.int32, device=dev)
     acc_all = ids_all = None
-    if use_dist and rank == 0:   # gather-to-root: only rank 0 receives the packed tiles
+    # the tile gather: over RCCL through the library's C ABI (rt_comm_init /
+    # rt_gather_tiles; torch.distributed only hands the communicator id around
+    # and times the run), or, on the gloo rehearsal path, torch's gather
+    native_gather = use_dist and backend == "nccl"
+    if native_gather:
+        uid = [rt.Context.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(world, rank, uid[0])
+    elif use_dist and rank == 0:   # gather-to-root: only rank 0 receives the packed tiles
         acc_all = torch.empty((world * lt * 64, 4), dtype=torch.float32, device=dev)
         ids_all = torch.empty((world * lt * 64,), dtype=torch.int32, device=dev)
     frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
@@ -272,7 +280,10 @@ def main():
         ctx.render_tiles(wl.mode, trav, rank, nsplit, 0, spp, acc_local.data_ptr(), ids_local.data_ptr())
         if events is not None:
             events[1].record(stream)
-        if use_dist:
+        if native_gather:   # one grouped RCCL receive per peer on rank 0, then the unpack
+            ctx.gather_tiles(W, H, acc_local.data_ptr(), ids_local.data_ptr(),
+                             frame.data_ptr() if rank == 0 else None, frame_ids.data_ptr() if rank == 0 else None)
+        elif use_dist:
             tiling.gather_tiles(dist, acc_local, ids_local, acc_all, ids_all)
             if rank == 0:
                 ctx.unpack_tiles(W, H, world, acc_all.data_ptr(), ids_all.data_ptr(), frame.data_ptr(),
@@ -362,6 +373,8 @@ def main():
                        "parallelism": f"tiles8x8/{nsplit}",
                        "world_size": dist.get_world_size() if use_dist else 1,
                        "backend": dist.get_backend() if use_dist else None,
+                       "gather": ("rt_gather_tiles (RCCL via the C ABI)" if native_gather else
+                                  "torch.distributed.gather (gloo)" if use_dist else None),
                        **({"share": f"rank 0 of {share} (profiling: this GPU's part of the {share}-GPU frame)"}
                           if share > 1 else {})},
             "roofline": roof,

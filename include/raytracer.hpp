@@ -160,6 +160,13 @@ public:
      * RGBA8 equirectangular texels, or nullptr for the constant environment */
     void set_environment_map(const uint8_t* rgba8, uint32_t width, uint32_t height);
     void reset_iteration();
+    /* Framebuffer tiling across the GPUs of a node: this state
+     * renders only rank `rank`'s interleaved 8x8 tiles of every frame
+     * (rt_render_tiles, into a packed accumulation kept across iterations) and
+     * gathers all ranks' tiles into rank 0's frame over RCCL (rt_comm_init with
+     * the communicator id rank 0 made, rt_gather_tiles).  Collective: every rank
+     * calls it, then render()/step() in lockstep; frame()/hit_ids() are rank 0's. */
+    void set_tiling(uint32_t nranks, uint32_t rank, const uint8_t comm_id[RT_COMM_ID_BYTES]);
 
     std::vector<float> frame() const;        /* linear RGBA32F accumulation, H x W x 4 */
     std::vector<uint32_t> hit_ids() const;   /* primary-hit triangle ids, H x W */
@@ -188,6 +195,11 @@ private:
     bool progressive_ = true;
     void* accum_ = nullptr;
     void* ids_ = nullptr;
+    void alloc_tiles();
+    uint32_t nranks_ = 1, rank_ = 0;   // set_tiling
+    bool tiled_ = false;
+    void* tile_accum_ = nullptr;       // this rank's packed tiles (rt_render_tiles)
+    void* tile_ids_ = nullptr;
 };
 
 }  // namespace raytracer

@@ -379,6 +379,39 @@ int rt_unpack_tiles(rt_ctx* ctx, uint32_t width, uint32_t height, uint32_t nrank
                     const float* packed_accum, const uint32_t* packed_ids,
                     float* frame_accum, uint32_t* frame_ids);
 
+/* ---- multi-GPU: the tile gather over RCCL -----------------
+ * One process per GPU, each with its own context: every rank renders its
+ * interleaved tiles (rt_render_tiles with rt_tileset {rank, nranks}), then
+ * rt_gather_tiles collects them on rank 0 -- one grouped RCCL receive of each
+ * peer's packed accumulation (16 B/px) and primary-hit ids (4 B/px), point to
+ * point over xGMI, no other collective -- and scatters them into rank 0's frame
+ * (rt_unpack_tiles).  Replaces, for a Rust host that tiles one
+ * RenderState::render (src/render_state.rs:483-561, driven per frame by
+ * src/lib.rs:331-363) across the GPUs of a node, what bench.py did with
+ * torch.distributed.  RCCL is loaded at rt_comm_init (librccl.so.1; a process
+ * that already holds one, e.g. through PyTorch, shares it). */
+#define RT_COMM_ID_BYTES 128u
+
+/* A new communicator id (ncclGetUniqueId), made on rank 0 and handed to every
+ * rank out of band (a file, a socket, the launcher's store). */
+int rt_comm_unique_id(uint8_t id[RT_COMM_ID_BYTES]);
+
+/* Join the communicator `id` as `rank` of `nranks` on the context's device
+ * (ncclCommInitRank; collective: every rank calls it).  One communicator per
+ * context; rt_comm_destroy (or rt_destroy) releases it. */
+int rt_comm_init(rt_ctx* ctx, uint32_t nranks, uint32_t rank, const uint8_t id[RT_COMM_ID_BYTES]);
+int rt_comm_destroy(rt_ctx* ctx);
+
+/* Gather the ranks' packed tiles of a width x height frame (each rank:
+ * rt_tileset_local_tiles(width, height, nranks) * 64 px in local_accum /
+ * local_ids, device pointers) to rank 0 and unpack them into rank 0's
+ * row-major frame_accum (W*H RGBA32F) and frame_ids (W*H u32); the other ranks
+ * pass NULL frames.  Collective over the context's communicator, asynchronous
+ * on the context's stream (RCCL runs on it); the frame is complete once the
+ * stream has drained.  Either id pointer may be NULL on every rank (accum only). */
+int rt_gather_tiles(rt_ctx* ctx, uint32_t width, uint32_t height, const float* local_accum,
+                    const uint32_t* local_ids, float* frame_accum, uint32_t* frame_ids);
+
 /* ---- ray queries: the walk alone ------------------------------------------ */
 
 /* One walk per ray through the context's BSP or BVH, with the render kernels'

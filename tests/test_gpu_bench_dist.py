@@ -4,8 +4,9 @@ device 0 (RT_BENCH_DEVICE=0) with the gloo backend (RCCL refuses two ranks on on
 GPU).  Each rank renders its interleaved 8x8 tiles (rt_render_tiles), the packed
 tiles are gathered to rank 0 (tiling.gather_tiles), rank 0 unpacks them
 (rt_unpack_tiles): the assembled frame equals the 1-rank frame bit for bit, and
-both equal the CPU oracle.  Only the RCCL transport itself is left to the 8-GPU
-node."""
+both equal the CPU oracle.  With RCCL (one rank on the box's GPU) the gather is
+the library's own (rt_gather_tiles, through the C ABI).  Only RCCL between
+GPUs is left to the 8-GPU node."""
 import json
 import os
 import socket
@@ -77,12 +78,14 @@ def test_eight_rank_bench_frame_equals_one_rank(tmp_path):
 def test_one_rank_rccl_bench_frame_equals_plain_run(tmp_path):
     # the driver's launch form with one process: torch.distributed.run opens an
     # RCCL ("nccl") process group on device 0 (bench.py init_process_group with
-    # device_id), the packed tiles go through tiling.gather_tiles' nccl branch
-    # (dist.gather of device tensors) and rt_unpack_tiles; the counters and times
-    # go through RCCL all_reduce.  The frame equals the plain 1-process run's.
+    # device_id), which hands rank 0's communicator id to the library
+    # (rt_comm_unique_id / rt_comm_init); the packed tiles go through the C ABI's
+    # RCCL gather and unpack (rt_gather_tiles); the counters and times go
+    # through torch's RCCL all_reduce.  The frame equals the plain 1-process run's.
     one, f1 = _bench(1, str(tmp_path / "n1.npz"))
     nc, fn = _bench(1, str(tmp_path / "nccl1.npz"), launcher=True, backend="nccl")
     assert nc["config"]["backend"] == "nccl" and nc["config"]["world_size"] == 1
+    assert nc["config"]["gather"].startswith("rt_gather_tiles")
     assert one["config"]["backend"] is None
     assert nc["rays_per_step"] == one["rays_per_step"]
     assert np.array_equal(f1["ids"], fn["ids"])

@@ -98,3 +98,20 @@ def test_project_subdivision_and_device_build(rt, tmp_path):
         assert np.array_equal(ids, rs.hit_ids())
     finally:
         rs.ctx.close()
+
+
+@pytest.mark.parametrize("scene,args", [("W7 E3 Cornell Box", ("--samples", "3")), ("W6 E1 Teapot", ())])
+def test_tiled_one_rank_communicator_equals_plain_frame(rt, tmp_path, scene, args):
+    # rt_render --nranks 1 --rank 0 --comm-file: the C++ RenderState renders its
+    # tiles (rt_render_tiles, packed accumulation across the progressive
+    # iterations) and gathers them through the library's RCCL communicator
+    # (rt_comm_unique_id published in a file, rt_comm_init, rt_gather_tiles):
+    # the frame equals the plain region render's bit for bit
+    plain = cpp_render(tmp_path, scene, 72, 40, *args)
+    tiled = cpp_render(tmp_path, scene, 72, 40, *args, "--nranks", "1", "--rank", "0", "--comm-file",
+                       str(tmp_path / "comm.id"))
+    assert os.path.getsize(tmp_path / "comm.id") == 128
+    for a, b in zip(plain[:3], tiled[:3]):
+        assert np.array_equal(a.view(np.uint32) if a.dtype == np.float32 else a,
+                              b.view(np.uint32) if b.dtype == np.float32 else b)
+    assert plain[3]["iteration"] == tiled[3]["iteration"]

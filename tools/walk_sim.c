@@ -19,6 +19,7 @@
 #include <math.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 
 typedef struct { float x, y, z; } v3;
 static v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
@@ -106,7 +107,9 @@ static double cert_margin(uint32_t node, v3 o, v3 d, const float* b)
     if (g_cert_floor_only == 2) return 1e30;
     g_cert_is_floor = den == fl;
     double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));
-    return 34 * u * d1 * w1 / den + 2 * u * d1 + 0x1p-20 * (om + g_cert_mag);
+    static double kscale = -1;
+    if (kscale < 0) { const char* e = getenv("WALK_CERT_K"); kscale = e ? atof(e) : 1.0; }
+    return kscale * 34 * u * d1 * w1 / den + 2 * u * d1 + 0x1p-20 * (om + g_cert_mag);
 }
 /* WALK_CELLS: n x 6 doubles, the box of the cells of the subtree's non-empty
  * leaves (the cells are the half-space intersections along the path: +-inf
