@@ -32,6 +32,7 @@ RT_OPT_SAMPLE_CHUNK = 4
 RT_OPT_SAMPLE_BUDGET_MB = 5
 RT_OPT_UNIT_ORDER = 6
 RT_OPT_BSP_CULL = 9
+RT_OPT_ASYNC_FOLD = 10
 RT_BSP_CULL_OFF, RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_FAST = range(3)
 RT_OPT_KERNEL_TIMING = 7
 RT_COMM_ID_BYTES = 128

@@ -112,6 +112,14 @@ struct rt_ctx {
     std::vector<hipEvent_t> kev;
     size_t kused = 0;   // events recorded since the last reset (2 per launch)
     // rt_comm_init: the tile gather's RCCL communicator (rt_gather_tiles)
+    // RT_OPT_ASYNC_FOLD: the fold and its consumers on a second stream, the
+    // per-sample scratch double-buffered (ev_free[b]: the fold that last read buffer b)
+    bool async_fold = false;
+    hipStream_t fold_stream = nullptr;
+    hipEvent_t ev_path = nullptr, ev_enter = nullptr, ev_fold = nullptr, ev_free[2] = {nullptr, nullptr};
+    DevBuf samples2;
+    uint32_t sbuf = 0;
+    bool fold_pending = false;   // work on fold_stream the context stream has not joined yet
     ncclComm_t comm = nullptr;
     uint32_t comm_nranks = 0, comm_rank = 0;
     DevBuf gather_accum, gather_ids;   // rank 0: every rank's packed tiles, rank-major
@@ -181,9 +189,40 @@ void build_recs(const std::vector<float>& pos, const std::vector<uint32_t>& idx,
     for (auto& t : th) t.join();
 }
 
+// The current device, without joining the fold stream (RT_OPT_ASYNC_FOLD): the
+// render calls and the fold's consumers, which order themselves against it.
+int set_dev_nojoin(rt_ctx* c)
+{
+    HIPCHK(c, hipSetDevice(c->device));
+    return RT_OK;
+}
+
+// The current device, with the fold stream's pending work joined into the
+// context stream first (every entry point but the renders and the fold's
+// consumers), so that synchronising the context stream covers it.
 int set_dev(rt_ctx* c)
 {
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->fold_pending) {
+        HIPCHK(c, hipEventRecord(c->ev_fold, c->fold_stream));
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_fold, 0));
+        c->fold_pending = false;
+    }
+    return RT_OK;
+}
+
+// The stream the fold's consumers (unpack, gather, sRGB frame) run on: the fold
+// stream under RT_OPT_ASYNC_FOLD, after the context stream's work so far.
+int out_stream(rt_ctx* c, hipStream_t* s)
+{
+    if (!c->async_fold || !c->fold_stream) {
+        *s = c->stream;
+        return RT_OK;
+    }
+    HIPCHK(c, hipEventRecord(c->ev_enter, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->fold_stream, c->ev_enter, 0));
+    c->fold_pending = true;
+    *s = c->fold_stream;
     return RT_OK;
 }
 
@@ -238,6 +277,9 @@ void rt_destroy(rt_ctx* c)
     (void)hipSetDevice(c->device);
     (void)hipDeviceSynchronize();
     (void)rt_comm_destroy(c);
+    for (hipEvent_t e : {c->ev_path, c->ev_enter, c->ev_fold, c->ev_free[0], c->ev_free[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (c->fold_stream) (void)hipStreamDestroy(c->fold_stream);
     for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
@@ -293,6 +335,16 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
     case RT_OPT_UNIT_ORDER:
         if (value < 0 || value > 1) return fail(c, RT_E_INVALID, "unit order must be 0 or 1");
         c->unit_order = (uint32_t)value;
+        return RT_OK;
+    case RT_OPT_ASYNC_FOLD:
+        if (value < 0 || value > 1) return fail(c, RT_E_INVALID, "async fold must be 0 or 1");
+        if (int r = set_dev(c)) return r;   // joins pending fold work
+        if (value && !c->fold_stream) {
+            HIPCHK(c, hipStreamCreateWithFlags(&c->fold_stream, hipStreamNonBlocking));
+            for (hipEvent_t* e : {&c->ev_path, &c->ev_enter, &c->ev_fold, &c->ev_free[0], &c->ev_free[1]})
+                HIPCHK(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+        }
+        c->async_fold = value != 0;
         return RT_OK;
     case RT_OPT_SAMPLE_BUDGET_MB:
         if (value < 1 || value > (1 << 20)) return fail(c, RT_E_INVALID, "sample budget must be in [1,2^20] MiB");
@@ -868,7 +920,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
             return fail(c, RT_E_NOT_READY, "rt_render: W6E1/PROJECT need the BSP root AABB");
     }
     if (!L.accum) return fail(c, RT_E_INVALID, "rt_render: accum buffer required");
-    if (int r = set_dev(c)) return r;
+    if (int r = set_dev_nojoin(c)) return r;
     const rtk::DevScene S = dev_scene(c);
     L.u = c->u;
     rtk::camera_basis(c->u, L.cam);
@@ -910,8 +962,14 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
         const uint64_t budget = c->sample_budget_mb << 20;
         uint32_t pass_spp = (uint32_t)std::min<uint64_t>(L.spp, std::max<uint64_t>(1, budget / per_it));
         const uint64_t need = per_it * pass_spp;
+        const bool async = c->async_fold && c->fold_stream;
         if (c->samples.n < need) HIPCHK(c, c->samples.alloc(need));
+        if (async && c->samples2.n < need) HIPCHK(c, c->samples2.alloc(need));
         L.samples = c->samples.as<float4>();
+        if (async) {   // the folds follow the context stream's work up to here
+            HIPCHK(c, hipEventRecord(c->ev_enter, c->stream));
+            HIPCHK(c, hipStreamWaitEvent(c->fold_stream, c->ev_enter, 0));
+        }
         const uint32_t first = L.first_iter, total = L.spp;
         for (uint32_t done = 0; done < total; done += pass_spp) {
             L.first_iter = first + done;
@@ -922,6 +980,21 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
             L.chunk = ch;
             L.unit_order = c->unit_order;
             L.nchunks = (L.spp + ch - 1) / ch;
+            if (async) {   // alternate scratch buffers: wait for the fold that last read this one
+                const uint32_t b = c->sbuf;
+                c->sbuf ^= 1u;
+                L.samples = (b ? c->samples2 : c->samples).as<float4>();
+                HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_free[b], 0));
+                HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
+                if (int r = launch_timed(c, S, L, mode, trav)) return r;
+                HIPCHK(c, hipEventRecord(c->ev_path, c->stream));
+                HIPCHK(c, hipStreamWaitEvent(c->fold_stream, c->ev_path, 0));
+                const int r = rtk::launch_fold(L, c->fold_stream);
+                if (r) return fail(c, r, std::string("fold launch failed: ") + hipGetErrorString(hipGetLastError()));
+                HIPCHK(c, hipEventRecord(c->ev_free[b], c->fold_stream));
+                c->fold_pending = true;
+                continue;
+            }
             HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
             if (int r = launch_timed(c, S, L, mode, trav)) return r;
             const int r = rtk::launch_fold(L, c->stream);
@@ -1036,10 +1109,12 @@ int rt_unpack_tiles(rt_ctx* c, uint32_t width, uint32_t height, uint32_t nranks,
                     const uint32_t* packed_ids, float* frame_accum, uint32_t* frame_ids)
 {
     if (!c || nranks == 0) return RT_E_INVALID;
-    if (int r = set_dev(c)) return r;
+    if (int r = set_dev_nojoin(c)) return r;
+    hipStream_t os;
+    if (int r = out_stream(c, &os)) return r;
     const uint32_t lt = rt_tileset_local_tiles(width, height, nranks);
     int r = rtk::launch_unpack(width, height, nranks, lt, reinterpret_cast<const float4*>(packed_accum), packed_ids,
-                               reinterpret_cast<float4*>(frame_accum), frame_ids, c->stream);
+                               reinterpret_cast<float4*>(frame_accum), frame_ids, os);
     if (r) return fail(c, r, "rt_unpack_tiles: launch failed");
     return RT_OK;
 }
@@ -1129,7 +1204,7 @@ int rt_comm_destroy(rt_ctx* c)
     if (!c) return RT_E_INVALID;
     if (!c->comm) return RT_OK;
     const Rccl& R = rccl();
-    (void)hipSetDevice(c->device);
+    (void)set_dev(c);   // joins a gather pending on the fold stream
     (void)hipStreamSynchronize(c->stream);
     ncclResult_t e = R.comm_destroy(c->comm);
     c->comm = nullptr;
@@ -1149,14 +1224,16 @@ int rt_gather_tiles(rt_ctx* c, uint32_t width, uint32_t height, const float* loc
     const bool root = me == 0;
     if (root && !frame_accum) return fail(c, RT_E_INVALID, "rt_gather_tiles: rank 0 needs frame_accum");
     if (root && local_ids && !frame_ids) return fail(c, RT_E_INVALID, "rt_gather_tiles: rank 0 needs frame_ids");
-    if (int r = set_dev(c)) return r;
+    if (int r = set_dev_nojoin(c)) return r;
+    hipStream_t os;   // the fold stream under RT_OPT_ASYNC_FOLD
+    if (int r = out_stream(c, &os)) return r;
     const Rccl& R = rccl();
     const size_t px = (size_t)rt_tileset_local_tiles(width, height, N) * 64u;
     if (!root) {
         // one group: this rank's accumulation and ids to rank 0
         ncclResult_t e = R.group_start();
-        if (!e) e = R.send(local_accum, px * 4, ncclFloat32, 0, c->comm, c->stream);
-        if (!e && local_ids) e = R.send(local_ids, px, ncclUint32, 0, c->comm, c->stream);
+        if (!e) e = R.send(local_accum, px * 4, ncclFloat32, 0, c->comm, os);
+        if (!e && local_ids) e = R.send(local_ids, px, ncclUint32, 0, c->comm, os);
         const ncclResult_t e2 = R.group_end();
         if (e || e2) return fail(c, RT_E_DEVICE, "rt_gather_tiles send: " + nccl_msg(R, e ? e : e2));
         return RT_OK;
@@ -1166,20 +1243,20 @@ int rt_gather_tiles(rt_ctx* c, uint32_t width, uint32_t height, const float* loc
     if (local_ids) HIPCHK(c, c->gather_ids.ensure(px * 4 * N));
     float* ga = c->gather_accum.as<float>();
     uint32_t* gi = c->gather_ids.as<uint32_t>();
-    HIPCHK(c, hipMemcpyAsync(ga, local_accum, px * 16, hipMemcpyDeviceToDevice, c->stream));
-    if (local_ids) HIPCHK(c, hipMemcpyAsync(gi, local_ids, px * 4, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(ga, local_accum, px * 16, hipMemcpyDeviceToDevice, os));
+    if (local_ids) HIPCHK(c, hipMemcpyAsync(gi, local_ids, px * 4, hipMemcpyDeviceToDevice, os));
     if (N > 1) {
         ncclResult_t e = R.group_start();
         for (uint32_t p = 1; p < N && !e; p++) {
-            e = R.recv(ga + p * px * 4, px * 4, ncclFloat32, (int)p, c->comm, c->stream);
-            if (!e && local_ids) e = R.recv(gi + p * px, px, ncclUint32, (int)p, c->comm, c->stream);
+            e = R.recv(ga + p * px * 4, px * 4, ncclFloat32, (int)p, c->comm, os);
+            if (!e && local_ids) e = R.recv(gi + p * px, px, ncclUint32, (int)p, c->comm, os);
         }
         const ncclResult_t e2 = R.group_end();
         if (e || e2) return fail(c, RT_E_DEVICE, "rt_gather_tiles recv: " + nccl_msg(R, e ? e : e2));
     }
     int r = rtk::launch_unpack(width, height, N, (uint32_t)(px / 64), reinterpret_cast<const float4*>(ga),
                                local_ids ? gi : nullptr, reinterpret_cast<float4*>(frame_accum),
-                               local_ids ? frame_ids : nullptr, c->stream);
+                               local_ids ? frame_ids : nullptr, os);
     if (r) return fail(c, r, "rt_gather_tiles: unpack launch failed");
     return RT_OK;
 }

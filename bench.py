@@ -35,6 +35,7 @@ L2_PEAK_GBS = 34500.0   # aggregate L2 (8 XCDs x 4 MiB), MI355X_MICROARCH.md "L2
 NUM_CUS, SIMDS_PER_CU, MAX_CLOCK_GHZ = 256, 4, 2.4
 VALU_PEAK_GINSTS = NUM_CUS * SIMDS_PER_CU * MAX_CLOCK_GHZ / 2.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+LIB_FOR_SHA = None   # the loaded lib02562rt.so (set in main once the package is imported)
 # SALU issue: the scalar ALU is one per-CU resource; tools/probes/issue_probe.hip
 # measured it saturating at 0.758 wave-instructions per shader cycle per CU
 # (profiles/r02/issue_probe.txt; the microarchitecture guide gives no figure)
@@ -95,8 +96,27 @@ def cpu_baseline(wl, trav, mesh, accel, spp, W, H, budget_s):
                       f"{W}x{H} frame, first {it} of its {spp} spp, {el:.1f} s"}
 
 
-def pmc_key(W, H, spp, trav, world, config):
-    return f"{W}x{H}x{spp}_{trav}_n{world}" + ("" if config == 3 else f"_c{config}")
+def pmc_key(W, H, spp, trav, world, config, cull=1):
+    return (f"{W}x{H}x{spp}_{trav}_n{world}" + ("" if config == 3 else f"_c{config}") +
+            {0: "_off", 1: "", 2: "_fast"}[cull if trav == "BSP" else 1])
+
+
+def fatbin_sha16(path):
+    """SHA-256 (16 hex digits) of the library's device code (.hip_fatbin section):
+    ties a committed PMC summary to the kernel build it was measured on."""
+    import hashlib
+    import struct
+    with open(path, "rb") as f:
+        b = f.read()
+    shoff, = struct.unpack_from("<Q", b, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    sec = [struct.unpack_from("<IIQQQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    stroff = sec[shstrndx][4]
+    for name, _t, _f, _a, off, size in sec:
+        end = b.index(b"\0", stroff + name)
+        if b[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(b[off:off + size]).hexdigest()[:16]
+    return None
 
 
 def roofline(key, kern_ms, alg_bytes, config, kernel):
@@ -117,12 +137,16 @@ def roofline(key, kern_ms, alg_bytes, config, kernel):
     if os.path.exists(PMC_SUMMARY):
         with open(PMC_SUMMARY) as f:
             pmc = json.load(f).get(key)
+    sha = fatbin_sha16(LIB_FOR_SHA) if LIB_FOR_SHA else None
     alg = {"bytes_per_launch": int(alg_bytes), "achieved": round(alg_bytes / s / 1e9, 1), "unit": "GB/s",
            "l2_peak": L2_PEAK_GBS, "l2_frac": round(alg_bytes / s / 1e9 / L2_PEAK_GBS, 4)}
     r = {"kernel": kernel, "kernel_ms": round(kern_ms, 3), "algorithmic": alg, "pmc": None, "traffic": None}
-    if pmc is None:
+    r["fatbin_sha16"] = sha
+    if pmc is None or (pmc.get("fatbin_sha16") and sha and pmc["fatbin_sha16"] != sha):
         r.update({"bound": "unmeasured", "achieved": None, "peak": None, "unit": None, "frac": None,
-                  "note": f"no PMC summary for {key} in profiles/pmc_summary.json"})
+                  "note": (f"no PMC summary for {key} in profiles/pmc_summary.json" if pmc is None else
+                           f"the PMC summary for {key} was measured on another kernel build "
+                           f"({pmc['fatbin_sha16']}, this one {sha})")})
         return r
     hbm_gbs = pmc["hbm_bytes_per_launch"] / s / 1e9
     valu = pmc["valu_insts_per_launch"] / s / 1e9
@@ -179,7 +203,11 @@ def main():
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)
-    ap.add_argument("--bsp-cull", type=int, default=None, help="RT_OPT_BSP_CULL (default 1: subtree culling on)")
+    ap.add_argument("--bsp-cull", type=int, default=None,
+                    help="RT_OPT_BSP_CULL: 0 off, 1 certified (the library default), 2 fast margin")
+    ap.add_argument("--async-fold", action="store_true",
+                    help="pipelined frames (RT_OPT_ASYNC_FOLD 1): a frame's fold and gather overlap the next "
+                         "frame's traversal kernel (measured slower on config 3: profiles/r04/ab_async_fold.txt)")
     ap.add_argument("--dump-frame", default=None,
                     help="rank 0 saves the last step's assembled frame (accum + ids) to this .npz")
     ap.add_argument("--progress", action="store_true",
@@ -224,6 +252,8 @@ def main():
     torch.cuda.set_stream(stream)
 
     rt = importlib.import_module("02562_raytracer_amd")   # after torch: shares its HIP runtime
+    global LIB_FOR_SHA
+    LIB_FOR_SHA = rt._ffi.LIB_PATH
     tiling = importlib.import_module("02562_raytracer_amd.tiling")
     wl = importlib.import_module("02562_raytracer_amd.configs").WORKLOADS[args.config]
     W, H = args.width or wl.width, args.height or wl.height
@@ -245,6 +275,8 @@ def main():
         ctx.set_option(rt._ffi.RT_OPT_UNIT_ORDER, args.unit_order)
     if args.bsp_cull is not None:
         ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, args.bsp_cull)
+    if args.async_fold:
+        ctx.set_option(rt._ffi.RT_OPT_ASYNC_FOLD, 1)
     ctx.upload_mesh(mesh)
     if trav == "BSP":
         accel = mesh.bsp_tree()
@@ -355,7 +387,8 @@ def main():
         # one GPU -- rank 0's, with rank 0's own kernel time and the PMC summary of
         # rank 0's share (profiles/pmc_summary.json key _n<N>, measured with --rank-share N)
         bytes_per_launch = rays[4] / (world if use_dist else 1) / max(1, launches_per_step)
-        roof = roofline(pmc_key(W, H, spp, trav, nsplit, args.config), kern_ms_own, bytes_per_launch, args.config,
+        cull = args.bsp_cull if args.bsp_cull is not None else rt._ffi.RT_BSP_CULL_CERTIFIED
+        roof = roofline(pmc_key(W, H, spp, trav, nsplit, args.config, cull), kern_ms_own, bytes_per_launch, args.config,
                         f"k_path<{wl.mode},{trav}>")
         roof["launches_per_step"] = launches_per_step
         roof["render_ms"] = round(render_ms, 3)
@@ -373,6 +406,7 @@ def main():
                        "parallelism": f"tiles8x8/{nsplit}",
                        "world_size": dist.get_world_size() if use_dist else 1,
                        "backend": dist.get_backend() if use_dist else None,
+                       "fold": "async (RT_OPT_ASYNC_FOLD)" if args.async_fold else "sync",
                        "gather": ("rt_gather_tiles (RCCL via the C ABI)" if native_gather else
                                   "torch.distributed.gather (gloo)" if use_dist else None),
                        **({"share": f"rank 0 of {share} (profiling: this GPU's part of the {share}-GPU frame)"}

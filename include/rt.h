@@ -173,6 +173,14 @@ typedef struct rt_ray_counts {
 /* option 8 is retired (trip-half postponement: slower on every BASELINE workload, and its
    per-trip test cost 1.7-4.4 % even when off, profiles/r02/sweep_KH_c5.txt, ab_nokh.txt) */
 #define RT_OPT_UNIT_ORDER      6  /* W7E3/W9E1 work-unit order: 0 chunk-major, 1 pixel-major (default) */
+#define RT_OPT_ASYNC_FOLD     10  /* 0 (default) / 1: pipelined frames.  The path tracers' progressive fold (the
+                                     last step of rt_render / rt_render_tiles) runs on a second, context-owned
+                                     stream, and so do the calls that consume its outputs (rt_unpack_tiles,
+                                     rt_gather_tiles, rt_frame_rgba8); the per-sample scratch is double-buffered.
+                                     The next render's traversal kernel then overlaps this frame's fold and
+                                     gather.  rt_synchronize, the memcpy/memset calls and every other entry point
+                                     wait for that stream first; a caller reading the outputs through its own
+                                     stream synchronizes the device (or calls rt_synchronize) first. */
 #define RT_OPT_BSP_CULL        9  /* subtree culling in the BSP walk: a subtree whose content
                                      box (the union of its triangles' bounding boxes), grown by a margin, the ray
                                      interval misses is skipped, and the walk's decisions use the interval clipped to

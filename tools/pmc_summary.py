@@ -58,6 +58,7 @@ if __name__ == "__main__":
     ap.add_argument("--out")
     ap.add_argument("--summary")
     ap.add_argument("--source", help="profiles/ path recorded as the summary's source")
+    ap.add_argument("--bench-json", help="the bench line of the same build: its roofline.fatbin_sha16 is recorded")
     a = ap.parse_args()
     res = load(a.dir, a.kernel)
     out = {k: {"counters": c, "derived": derived(c)} for k, c in res.items()}
@@ -78,6 +79,9 @@ if __name__ == "__main__":
                "valu_insts_per_launch": int(c["SQ_INSTS_VALU"])}
         if "SQ_INSTS_SALU" in c:
             ent["salu_insts_per_launch"] = int(c["SQ_INSTS_SALU"])
+        if a.bench_json:
+            line = [l for l in open(a.bench_json) if l.startswith("{")][-1]
+            ent["fatbin_sha16"] = json.loads(line)["roofline"].get("fatbin_sha16")
         for k in ("l2_hit_rate", "valu_lane_util", "wait_frac", "salu_per_valu", "l1_hit_rate"):
             if k in d:
                 ent[k] = round(d[k], 4)

@@ -83,10 +83,11 @@ double walk_sim_cert_mean(void) { return g_cert_margin_n ? g_cert_margin_sum / g
 static int g_cert_is_floor = 0;
 double g_lost[4];
 void walk_sim_lost(double* o) { for (int i = 0; i < 4; i++) o[i] = g_lost[i]; }
-static double cert_margin(uint32_t node, v3 o, v3 d, const float* b)
+static double cert_margin_c(const double* c, v3 o, v3 d, const float* b);
+static double cert_margin(uint32_t node, v3 o, v3 d, const float* b) { return cert_margin_c(g_cert + 7 * (size_t)node, o, d, b); }
+static double cert_margin_c(const double* c, v3 o, v3 d, const float* b)
 {
     const double u = 0x1p-24;
-    const double* c = g_cert + 7 * (size_t)node;
     double E2 = c[0];
     double w1 = fabs(d.x) + fabs(d.y) + fabs(d.z);
     double d1 = 0;
@@ -254,12 +255,48 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
                                         if (x > bb[3 + a]) bb[3 + a] = x;
                                     }
                             }
-                            for (int a = 0; a < 3; a++) { bb[a] -= g_chunk_margin; bb[3 + a] += g_chunk_margin; }
                             st[S_LT] += g_chunk_free ? 0 : 1;
-                            const float* sv = g_boxes;
-                            g_boxes = bb;
-                            int miss = box_miss(0, o, d, tmin, tmax);
-                            g_boxes = sv;
+                            int miss;
+                            if (g_cert) {
+                                /* the run's certification data, as the repack would store it */
+                                double c7[7] = {0, INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+                                for (uint32_t q = j; q < e; q++) {
+                                    const uint32_t* ix = s->idx + 4 * (size_t)s->ids[first + q];
+                                    v3 p0 = V(s->pos[4 * ix[0]], s->pos[4 * ix[0] + 1], s->pos[4 * ix[0] + 2]);
+                                    v3 p1 = V(s->pos[4 * ix[1]], s->pos[4 * ix[1] + 1], s->pos[4 * ix[1] + 2]);
+                                    v3 p2 = V(s->pos[4 * ix[2]], s->pos[4 * ix[2] + 1], s->pos[4 * ix[2] + 2]);
+                                    v3 e0 = sub(p1, p0), e1 = sub(p2, p0);
+                                    double nn[3] = {(double)e0.y * e1.z - (double)e0.z * e1.y, (double)e0.z * e1.x - (double)e0.x * e1.z,
+                                                    (double)e0.x * e1.y - (double)e0.y * e1.x};
+                                    double E = fmax(fmax(fmax(fabs(e0.x), fabs(e0.y)), fabs(e0.z)), fmax(fmax(fabs(e1.x), fabs(e1.y)), fabs(e1.z)));
+                                    if (E * E > c7[0]) c7[0] = E * E;
+                                    for (int a = 0; a < 3; a++) {
+                                        if (nn[a] < c7[1 + a]) c7[1 + a] = nn[a];
+                                        if (nn[a] > c7[4 + a]) c7[4 + a] = nn[a];
+                                    }
+                                }
+                                if (c7[0] > 0)
+                                    for (int a = 1; a < 7; a++) c7[a] /= c7[0];
+                                else
+                                    for (int a = 1; a < 7; a++) c7[a] = 0, c7[0] = 1;
+                                double m = cert_margin_c(c7, o, d, bb);
+                                double t0 = tmin, t1 = tmax;
+                                for (int k = 0; k < 3; k++) {
+                                    double dk = comp(d, k), ok = comp(o, k);
+                                    if (fabs(dk) < 1e-8) continue;
+                                    double a = (bb[k] - m - ok) / dk, cc = (bb[3 + k] + m - ok) / dk;
+                                    if (a > cc) { double x = a; a = cc; cc = x; }
+                                    if (a > t0) t0 = a;
+                                    if (cc < t1) t1 = cc;
+                                }
+                                miss = t0 > t1 + (fabs(t0) + fabs(t1)) * 0x1p-18;
+                            } else {
+                                for (int a = 0; a < 3; a++) { bb[a] -= g_chunk_margin; bb[3 + a] += g_chunk_margin; }
+                                const float* sv = g_boxes;
+                                g_boxes = bb;
+                                miss = box_miss(0, o, d, tmin, tmax);
+                                g_boxes = sv;
+                            }
                             if (miss) { j = e; continue; }
                         }
                         st[S_LT] += 1;

@@ -89,6 +89,17 @@ def main():
             flags.append(int(rng.random() < 0.5))
     R = np.ascontiguousarray(np.array(rays, np.float32))
     F = np.ascontiguousarray(np.array(flags, np.uint32))
+    if os.environ.get("WALK_RAYS"):   # 0: camera rays only, 1: shadow, 2: bounce (the list's 3-ray groups)
+        kind = np.zeros(len(R), int)
+        i = 0
+        while i < len(R):   # camera ray, then its shadow + bounce when it hit
+            if i + 2 < len(R) and F[i + 1] == 1:
+                kind[i + 1], kind[i + 2] = 1, 2
+                i += 3
+            else:
+                i += 1
+        keep = kind == int(os.environ["WALK_RAYS"])
+        R, F = np.ascontiguousarray(R[keep]), np.ascontiguousarray(F[keep])
     out = np.zeros(50, np.float64)
     # content boxes of every node's subtree (v3), bottom-up from the leaves' triangles
     boxes = None
