@@ -90,6 +90,10 @@ struct rt_ctx {
     uint32_t bsp_depth = 0;
     float aabb[6] = {0, 0, 0, 0, 0, 0};
     bool has_bsp = false;
+    // the treelets' camera terms (rtk::launch_bsp_camera) are for this eye
+    bool hcam_valid = false;
+    float hcam_eye[3] = {0, 0, 0};
+    DevBuf hcam_scratch;
     DevBuf bvh_nodes, bvh_ids;   // bvh_nodes: [32-B nodes | 48-B records]
     DevBuf bvh_ref;              // the GpuNode array in the reference layout (rt_download_bvh)
     uint32_t bvh_rec_off = 0;
@@ -492,6 +496,7 @@ int rt_upload_mesh(rt_ctx* c, const float* pos_vec4, const float* nrm_vec4, uint
 // the BSP's root box (bsp_box_miss in rt_kernels.hip adds the ray origin's).
 static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off, size_t total, const float aabb[8])
 {
+    c->hcam_valid = false;
     HIPCHK(c, c->bsp_nodes.alloc(total));
     DevBuf boxes;
     HIPCHK(c, boxes.alloc((size_t)nnodes * 64));
@@ -835,10 +840,28 @@ int rt_set_environment_map(rt_ctx* c, const uint8_t* rgba8, uint32_t width, uint
 }
 
 // The device-resident scene as the kernels read it (rt_internal.h DevScene).
+// The camera terms of the treelets for the uniforms' eye (certified culling,
+// rt_bsp_build.hip launch_bsp_camera): recomputed when the eye moves.
+static int ensure_hcam(rt_ctx* c)
+{
+    if (!c->has_bsp || !c->has_u || c->bsp_cull != RT_BSP_CULL_CERTIFIED) return RT_OK;
+    const float* e = c->u.camera_pos;
+    if (c->hcam_valid && memcmp(e, c->hcam_eye, sizeof c->hcam_eye) == 0) return RT_OK;
+    if (!(std::isfinite(e[0]) && std::isfinite(e[1]) && std::isfinite(e[2]))) return RT_OK;
+    HIPCHK(c, c->hcam_scratch.ensure((size_t)c->bsp_nnodes * 4));
+    if (rtk::launch_bsp_camera(c->bsp_ref_tree.as<uint32_t>(), c->bsp_nnodes, c->pos.as<float4>(), c->idx.as<uint4>(),
+                               c->bsp_ids.as<uint32_t>(), c->bsp_nids, e, c->bsp_nodes.p, c->hcam_scratch.p, c->stream))
+        return fail(c, RT_E_DEVICE, "BSP camera terms: launch failed");
+    memcpy(c->hcam_eye, e, sizeof c->hcam_eye);
+    c->hcam_valid = true;
+    return RT_OK;
+}
+
 static rtk::DevScene dev_scene(const rt_ctx* c)
 {
     rtk::DevScene S;
     memset(&S, 0, sizeof S);
+    for (int k = 0; k < 3; k++) S.cam_eye[k] = c->hcam_valid ? c->hcam_eye[k] : NAN;
     S.pos = c->pos.as<float4>();
     S.nrm = c->nrm.as<float4>();
     S.tri_idx = c->idx.as<uint4>();
@@ -893,6 +916,8 @@ int rt_trace_rays(rt_ctx* c, rt_traverse trav, const float* rays, const uint32_t
         if (c->bvh_deep.n < need) HIPCHK(c, c->bvh_deep.alloc(need));
         deep = c->bvh_deep.as<uint32_t>();
     }
+    if (trav == RT_TRAVERSE_BSP)
+        if (int rr = ensure_hcam(c)) return rr;
     const int r = rtk::launch_query(dev_scene(c), trav, rays, flags, n, hits, deep, c->num_cus, c->stream);
     if (r) return fail(c, r, std::string("rt_trace_rays: launch failed: ") + hipGetErrorString(hipGetLastError()));
     return RT_OK;
@@ -921,6 +946,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     }
     if (!L.accum) return fail(c, RT_E_INVALID, "rt_render: accum buffer required");
     if (int r = set_dev_nojoin(c)) return r;
+    if (int r = ensure_hcam(c)) return r;
     const rtk::DevScene S = dev_scene(c);
     L.u = c->u;
     rtk::camera_basis(c->u, L.cam);

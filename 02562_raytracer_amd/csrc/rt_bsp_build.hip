@@ -527,8 +527,9 @@ __device__ __forceinline__ uint32_t h_ru(float x) { return __half_as_ushort(__fl
 // -- node M's content box, expanded by `margin` on every side, the 8-B nodes a
 // three-level walk from M reads (interior {axis, plane bits}; leaf {3 |
 // (48*count) << 2, byte offset of its first record}), and the certification
-// data: F = 1e-10 / E2 rounded down (+inf for a subtree without a triangle of
-// non-zero extent), and the normal box divided by E2 (|x| <= 2: |n*_i| <=
+// data: F = 1e-10 / E2 rounded down to a bf16 (+inf for a subtree without a
+// triangle of non-zero extent) with the camera term H (bf16, k_treelet_hcam)
+// in the same dword, and the normal box divided by E2 (|x| <= 2: |n*_i| <=
 // 2 E2) as its centre c (f16, nearest) and radius r (f16, rounded up, so that
 // the box lies inside [c - r, c + r]).
 __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes,
@@ -577,7 +578,9 @@ __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const 
                 hb[3 + k] = h_ru(f_ru(r * (1.0 + 0x1p-40)));
             }
         }
-        o[20] = __float_as_uint(F);
+        // F as a bf16 (the float's high half: truncation, i.e. rounded down for a
+        // positive F); the high half is the camera term H (k_treelet_hcam), 0 until set
+        o[20] = __float_as_uint(F) >> 16;
         o[21] = hb[0] | (hb[1] << 16);
         o[22] = hb[2] | (hb[3] << 16);
         o[23] = hb[4] | (hb[5] << 16);
@@ -597,6 +600,81 @@ __global__ void __launch_bounds__(256) k_tri_records2(const float4* pos, const u
         recs[3u * k + 1u] = make_float4(e0[1], e0[2], e1[0], e1[1]);
         recs[3u * k + 2u] = make_float4(e1[2], n[0], n[1], n[2]);
     }
+}
+
+// The camera term of the certified margin (rt_kernels.hip bsp_box_miss,
+// DESIGN.md section 4 "Certified culling"): for the eye E of the camera rays,
+// H = min over a subtree's triangles of |(v0 - E) . n*| / E_T^2, a lower bound,
+// rounded down (the f64 dot product's error subtracted, a 2^-19 relative slack
+// for the kernel's f32 evaluation).  A triangle whose edges are zero cannot be
+// accepted (its denominator is 0) and constrains nothing (+inf).
+__device__ __forceinline__ float tri_hcam(const float4 v[3], const double E[3])
+{
+    const float e0[3] = {v[1].x - v[0].x, v[1].y - v[0].y, v[1].z - v[0].z};
+    const float e1[3] = {v[2].x - v[0].x, v[2].y - v[0].y, v[2].z - v[0].z};
+    const double n[3] = {(double)e0[1] * e1[2] - (double)e0[2] * e1[1], (double)e0[2] * e1[0] - (double)e0[0] * e1[2],
+                         (double)e0[0] * e1[1] - (double)e0[1] * e1[0]};
+    const double Em = fmax(fmax(fmax(fabs((double)e0[0]), fabs((double)e0[1])), fabs((double)e0[2])),
+                           fmax(fmax(fabs((double)e1[0]), fabs((double)e1[1])), fabs((double)e1[2])));
+    if (!(Em > 0.0)) return INFINITY;
+    const double d[3] = {(double)v[0].x - E[0], (double)v[0].y - E[1], (double)v[0].z - E[2]};
+    const double dot = d[0] * n[0] + d[1] * n[1] + d[2] * n[2];
+    const double err = 0x1p-45 * (fabs(d[0] * n[0]) + fabs(d[1] * n[1]) + fabs(d[2] * n[2]));
+    const double eta = fabs(dot) - err;
+    if (!(eta > 0.0)) return 0.0f;
+    return f_rd(eta / (Em * Em) * (1.0 - 0x1p-19));
+}
+__global__ void __launch_bounds__(256) k_leaf_hcam(const uint32_t* tree, uint32_t nnodes, const float4* pos,
+                                                   const uint4* idx, const uint32_t* ids, uint32_t nids, double ex,
+                                                   double ey, double ez, float* h)
+{
+    const double E[3] = {ex, ey, ez};
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nnodes; i += gridDim.x * 256u) {
+        const uint32_t n0 = tree[4 * (size_t)i], first = tree[4 * (size_t)i + 1];
+        float m = INFINITY;
+        const uint32_t cnt = (n0 & 3u) == 3u ? n0 >> 2 : 0u;
+        if ((uint64_t)first + cnt <= nids)
+            for (uint32_t k = 0; k < cnt; k++) {
+                const uint4 ix = idx[ids[first + k]];
+                const float4 v[3] = {pos[ix.x], pos[ix.y], pos[ix.z]};
+                m = fminf(m, tri_hcam(v, E));
+            }
+        h[i] = m;
+    }
+}
+__global__ void __launch_bounds__(256) k_node_hcam(const uint32_t* tree, uint32_t nnodes, uint32_t lo_i, uint32_t hi_i,
+                                                   float* h)
+{
+    for (uint32_t i = lo_i + blockIdx.x * 256u + threadIdx.x; i < hi_i; i += gridDim.x * 256u) {
+        if ((tree[4 * (size_t)i] & 3u) == 3u || 2ull * i + 2 >= nnodes) continue;
+        h[i] = fminf(h[2 * (size_t)i + 1], h[2 * (size_t)i + 2]);
+    }
+}
+// the bf16 of H (truncated: rounded down) into the high half of treelet M's q5.x
+__global__ void __launch_bounds__(256) k_treelet_hcam(const float* h, uint32_t nnodes, uint32_t* tl)
+{
+    constexpr uint32_t W = BSP_TREELET_BYTES / 4;
+    for (size_t m = 1 + (size_t)blockIdx.x * 256u + threadIdx.x; m <= nnodes; m += (size_t)gridDim.x * 256u) {
+        uint32_t* o = tl + W * m + 20;
+        *o = (*o & 0xFFFFu) | (__float_as_uint(h[m - 1]) & 0xFFFF0000u);
+    }
+}
+int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, const uint4* idx, const uint32_t* ids,
+                      uint32_t nids, const float eye[3], void* blob, void* scratch, hipStream_t s)
+{
+    float* h = reinterpret_cast<float*>(scratch);
+    const uint32_t g0 = std::min<uint32_t>(16384, (nnodes + 255) / 256);
+    hipLaunchKernelGGL(k_leaf_hcam, dim3(g0), dim3(256), 0, s, tree, nnodes, pos, idx, ids, nids, (double)eye[0],
+                       (double)eye[1], (double)eye[2], h);
+    uint32_t depth = 0;
+    while ((2ull << depth) - 1 < nnodes) depth++;
+    for (int d = (int)depth - 1; d >= 0; d--) {
+        const uint32_t lo = (1u << d) - 1u, hi = std::min<uint32_t>(nnodes, (2u << d) - 1u);
+        const uint32_t g = std::min<uint32_t>(16384, (hi - lo + 255) / 256);
+        hipLaunchKernelGGL(k_node_hcam, dim3(g), dim3(256), 0, s, tree, nnodes, lo, hi, h);
+    }
+    hipLaunchKernelGGL(k_treelet_hcam, dim3(g0), dim3(256), 0, s, h, nnodes, reinterpret_cast<uint32_t*>(blob));
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }
 
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,

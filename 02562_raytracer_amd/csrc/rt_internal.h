@@ -49,6 +49,9 @@ struct DevScene {
     // fast (RT_BSP_CULL_FAST): k1 = k3 = 0, ko = 2^-10, bsp_margin = 2^-10 x scene
     float bsp_margin;
     float cull_k1, cull_k3, cull_ko;
+    // the eye the treelets' camera terms are for (rt_bsp_build.hip
+    // launch_bsp_camera): rays starting exactly there use them (NaN: none)
+    float cam_eye[3];
 };
 
 // Work mapping + outputs of one launch.
@@ -133,6 +136,9 @@ int build_bsp_device(const float4* pos, const uint4* idx, uint32_t ntris, uint32
 // then the 48-B records; box_scratch: nnodes x 64 B of device memory for the
 // content boxes and the certification data
 constexpr uint32_t BSP_TREELET_BYTES = 96;
+// the camera term H of every treelet for the camera-ray eye (scratch: nnodes floats)
+int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, const uint4* idx, const uint32_t* ids,
+                      uint32_t nids, const float eye[3], void* blob, void* scratch, hipStream_t stream);
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
                       const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,
                       void* box_scratch, hipStream_t stream);

@@ -635,7 +635,8 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 //   m = D1 * (k1 * w1 / max(F, 2 Dlb - 20u w1) + k3) + max(|o|inf * ko, dscene)
 // with D1 >= |v0 - o|_1 for every point v0 of the box, w1 = |w|_1, F = 1e-10 /
 // E2 and 2 Dlb a lower bound of |w . n*| / E2 over the subtree's normals from
-// the treelet's normal box (q5: centre and radius of n* / E2).  Certified mode (k1 = 36u, k3 = 2u, ko and
+// the treelet's normal box (q5: centre and radius of n* / E2); for a camera ray
+// also a bound from how far the eye is from its triangles' planes (q5's H).  Certified mode (k1 = 36u, k3 = 2u, ko and
 // dscene 2^-19 of the magnitudes): m bounds the L-inf distance from the box of
 // every point o + dist*w where intersect_triangle (w7e3.wgsl:286-332) can
 // accept one of the subtree's triangles -- its f32 rounding, including
@@ -684,7 +685,18 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
     const float wr = __builtin_fmaf(rt_absf(w.z), h2f(q5.w >> 16),
                                     __builtin_fmaf(rt_absf(w.y), h2f(q5.w & 0xFFFFu), rt_absf(w.x) * h2f(q5.z >> 16)));
     const float dlb2 = rt_absf(wc) - wr;
-    const float den = __builtin_fmaxf(__uint_as_float(q5.x), dlb2 - (20.0f * 0x1p-24f) * w1);
+    float den = __builtin_fmaxf(__uint_as_float(q5.x << 16), dlb2 - (20.0f * 0x1p-24f) * w1);
+    // a camera ray (its origin is the eye the treelets' camera terms H are for):
+    // |denom| / E_T^2 >= ((H - 14u D1) |w|inf - 38u D1 w1) / Dinf, Dinf >= |x - o|inf
+    // over the box (DESIGN.md section 4 "Certified culling", the camera bound)
+    const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
+    const float Dinf = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(rt_absf(dl[0]), rt_absf(dh[0])),
+                                                       __builtin_fmaxf(rt_absf(dl[1]), rt_absf(dh[1]))),
+                                       __builtin_fmaxf(rt_absf(dl[2]), rt_absf(dh[2])));
+    const float winf = __builtin_fmaxf(__builtin_fmaxf(rt_absf(w.x), rt_absf(w.y)), rt_absf(w.z));
+    const float H = __uint_as_float(q5.x & 0xFFFF0000u);
+    const float dcam = ((H - (14.0f * 0x1p-24f) * D1) * winf - (38.0f * 0x1p-24f) * D1 * w1) * __builtin_amdgcn_rcpf(Dinf);
+    den = __builtin_fmaxf(den, cam ? dcam : 0.0f);
     const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
     const float m = D1 * (S.cull_k1 * w1 * __builtin_amdgcn_rcpf(den) + S.cull_k3) +
                     __builtin_fmaxf(mo * S.cull_ko, S.bsp_margin);

@@ -15,11 +15,17 @@
  * distance of Q from the box in units of m (it must stay below 1), with Q
  * evaluated in long double.
  * Build: gcc -O2 -ffp-contract=off -o cert_bound cert_bound.c -lm
- * usage: cert_bound <trials> <seed> [scene magnitude]   prints: accepts max_ratio floor_accepts */
+ * usage: cert_bound <trials> <seed> [camera 0/1]   prints: accepts max_ratio floor_accepts
+ * With camera 1 the margin also takes the camera bound (rt_kernels.hip bsp_box_miss)
+ * with each ray's origin as the eye -- every trial is then a camera ray. */
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+
+static int g_cam = 0;
+static long g_cam_binds = 0;   /* accepts whose margin the camera bound set */   /* argv[3] = 1: the camera bound too, with every ray's origin as the eye */
 
 typedef struct { float x, y, z; } v3;
 static v3 V(float x, float y, float z) { v3 r = {x, y, z}; return r; }
@@ -102,6 +108,27 @@ static float cert_margin(v3 v0, v3 v1, v3 v2, v3 o, v3 w, float scene, float bmi
     float wr = fmaf(fabsf(w.z), rr[2], fmaf(fabsf(w.y), rr[1], fabsf(w.x) * rr[0]));
     float dlb2 = fabsf(wc) - wr;
     float den = fmaxf(F, dlb2 - (20.0f * 0x1p-24f) * w1);
+    if (g_cam) {
+        /* the camera bound, with the ray's origin as the eye: H = |(v0 - o) . n*| / E2
+         * rounded down (rt_bsp_build.hip tri_hcam), bf16-truncated as the treelet stores it */
+        double dd[3] = {(double)v0.x - o.x, (double)v0.y - o.y, (double)v0.z - o.z};
+        double dot = dd[0] * n[0] + dd[1] * n[1] + dd[2] * n[2];
+        double err = 0x1p-45 * (fabs(dd[0] * n[0]) + fabs(dd[1] * n[1]) + fabs(dd[2] * n[2]));
+        double eta = fabs(dot) - err;
+        float H = E2 > 0 ? (eta > 0 ? (float)(eta / E2 * (1.0 - 0x1p-19)) : 0.0f) : INFINITY;
+        H = nextafterf(H, 0.0f);
+        uint32_t hb;
+        memcpy(&hb, &H, 4);
+        hb &= 0xFFFF0000u;
+        memcpy(&H, &hb, 4);
+        float Dinf = 0.0f;
+        for (int a = 0; a < 3; a++) Dinf = fmaxf(Dinf, fmaxf(fabsf(bmin[a] - oo[a]), fabsf(bmax[a] - oo[a])));
+        float winf = fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fabsf(w.z));
+        float rc = nextafterf(1.0f / Dinf, INFINITY);   /* v_rcp_f32 within 1 ulp: the worse side here */
+        float dcam = ((H - (14.0f * 0x1p-24f) * D1) * winf - (38.0f * 0x1p-24f) * D1 * w1) * rc;
+        if (dcam > den) g_cam_binds++;
+        den = fmaxf(den, dcam);
+    }
     float mo = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     /* v_rcp_f32 is within 1 ulp: emulate the worse side */
     float rc = nextafterf(1.0f / den, 0.0f);
@@ -112,6 +139,7 @@ int main(int argc, char** argv)
 {
     long trials = argc > 1 ? atol(argv[1]) : 1000000;
     st ^= (uint64_t)(argc > 2 ? atol(argv[2]) : 1) * 0x2545F4914F6CDD1Dull;
+    g_cam = argc > 3 ? atoi(argv[3]) : 0;
     long acc = 0, floor_acc = 0;
     double worst = 0.0;
     for (long it = 0; it < trials; it++) {
@@ -168,6 +196,6 @@ int main(int argc, char** argv)
         double ratio = (double)(dd / m);
         if (ratio > worst) worst = ratio;
     }
-    printf("%ld %.6g %ld\n", acc, worst, floor_acc);
+    printf("%ld %.6g %ld %ld\n", acc, worst, floor_acc, g_cam_binds);
     return 0;
 }

@@ -108,3 +108,67 @@ def test_grazing_rays_default_walk_equals_oracle(rt, gpu, oracle, scene):
             off.append(float(np.max(np.maximum(v.min(0) - p, p - v.max(0)))))
         print(f"  ray {i}: hits {h['OFF']['tri'][i]} / {fast['tri'][i]}, off-box {off}, margin {m:.3g}")
         assert off and max(off) > m, (i, off, m)
+
+
+@pytest.mark.parametrize("scene", ["soup", "bunny"])
+def test_camera_rays_default_walk_equals_oracle(rt, gpu, oracle, scene):
+    # rays from the camera eye, which take the camera bound of the certified margin
+    # (the treelets' per-eye terms): aimed at points of the triangles whose planes
+    # pass closest to the eye -- the silhouette, where camera rays graze -- and at
+    # random points of the frame; every ray starts exactly at the eye
+    mesh = rt.Mesh.synth_soup(1_000_000) if scene == "soup" else rt.Mesh.synth_bunny()
+    V, N, I, M, L = mesh.arrays()
+    eye = np.array([0.0, 0.0, 3.0] if scene == "soup" else [-0.02, 0.11, 0.6], np.float32)
+    P = V[:, :3].astype(np.float64)
+    v0, v1, v2 = P[I[:, 0]], P[I[:, 1]], P[I[:, 2]]
+    n = np.cross(v1 - v0, v2 - v0)
+    ln = np.linalg.norm(n, axis=1)
+    ok = ln > 0
+    h = np.full(len(I), np.inf)
+    h[ok] = np.abs(np.sum((v0[ok] - eye) * n[ok], axis=1)) / ln[ok]
+    edge_on = np.argsort(h)[:200_000]
+    rng = np.random.default_rng(23)
+    t = np.concatenate([edge_on, rng.integers(len(I), size=100_000)])
+    u, v = rng.random(len(t)), rng.random(len(t))
+    flip = u + v > 1
+    u[flip], v[flip] = 1 - u[flip], 1 - v[flip]
+    # points on the triangle, and just beside it in its plane (misses that graze it)
+    s = np.where(rng.random(len(t)) < 0.5, 1.0, 1.0 + 10.0 ** rng.uniform(-4, -1, len(t)))
+    p = v0[t] + (u * s)[:, None] * (v1[t] - v0[t]) + (v * s)[:, None] * (v2[t] - v0[t])
+    w = p - eye
+    w /= np.linalg.norm(w, axis=1)[:, None]
+    R = np.concatenate([np.tile(eye, (len(t), 1)), w, np.full((len(t), 1), 1e-4), np.full((len(t), 1), 5000.0)],
+                       axis=1).astype(np.float32)
+    R[:, :3] = eye   # exactly the eye
+    anyhit = np.zeros(len(R), bool)
+    ctx = rt.Context(0)
+    bsp = mesh.bsp_tree()
+    try:
+        ctx.upload_mesh(mesh)
+        ctx.upload_bsp(bsp)
+        ctx.set_uniforms(rt.make_uniform(tuple(float(x) for x in eye), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 1.5, 64, 64))
+        h_ = {}
+        for name in ("OFF", "FAST", "CERTIFIED"):
+            ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, getattr(rt._ffi, "RT_BSP_CULL_" + name))
+            ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
+            h_[name] = ctx.trace_rays("BSP", R, anyhit)
+    finally:
+        ctx.close()
+    MISS = 0xFFFFFFFF
+    tree, planes, ids, aabb, D = bsp.arrays()
+    om = types.SimpleNamespace(pos=np.ascontiguousarray(V), nrm=np.ascontiguousarray(N), idx=np.ascontiguousarray(I),
+                               ntris=I.shape[0], mats=np.ascontiguousarray(M), lights=np.ascontiguousarray(L))
+    sc = oracle.SceneRef(om, types.SimpleNamespace(aabb=aabb, tree=tree, planes=planes, ids=ids, max_depth=D))
+    otri, odist = oracle.trace_many(sc, "BSP", R)
+    cert = h_["CERTIFIED"]
+    bad = (cert["tri"] != otri) | ((otri != MISS) & (cert["dist"].view(np.uint32) != odist.view(np.uint32)))
+    hits = int((otri != MISS).sum())
+    badf = np.zeros(len(R), bool)
+    for k in ("tri", "dist", "beta", "gamma"):
+        badf |= h_["OFF"][k].view(np.uint32) != h_["FAST"][k].view(np.uint32)
+    print(f"{scene}: {len(R)} camera rays ({hits} hits): certified vs oracle {int(bad.sum())} differ, "
+          f"fast vs unculled {int(badf.sum())} differ")
+    assert hits > len(R) // 4
+    assert bad.sum() == 0
+    for k in ("tri", "dist", "beta", "gamma"):
+        assert np.array_equal(h_["OFF"][k].view(np.uint32), cert[k].view(np.uint32)), k

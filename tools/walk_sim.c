@@ -81,6 +81,12 @@ void walk_sim_cert(const double* c, double mag, int floor_only) { g_cert = c; g_
 double g_cert_margin_sum = 0, g_cert_margin_n = 0;
 double walk_sim_cert_mean(void) { return g_cert_margin_n ? g_cert_margin_sum / g_cert_margin_n : 0; }
 static int g_cert_is_floor = 0;
+/* WALK_CAM: per node min over the subtree's triangles of |(v0 - E) . n*| / E_T^2 for the
+ * camera eye E (camera rays start at E: the accept point must then be near the plane of
+ * the triangle *and* the eye off it, which bounds |denom| below) */
+static const double* g_hcam = 0;
+static v3 g_eye;
+void walk_sim_cam(const double* h, float ex, float ey, float ez) { g_hcam = h; g_eye = V(ex, ey, ez); }
 double g_lost[4];
 void walk_sim_lost(double* o) { for (int i = 0; i < 4; i++) o[i] = g_lost[i]; }
 static double cert_margin_c(const double* c, v3 o, v3 d, const float* b);
@@ -105,6 +111,17 @@ static double cert_margin_c(const double* c, v3 o, v3 d, const float* b)
     double den = 2 * dlb - 32 * u * w1;
     double fl = 1e-10 / E2;
     if (g_cert_floor_only || den < fl) den = fl;
+    if (g_hcam && o.x == g_eye.x && o.y == g_eye.y && o.z == g_eye.z) {
+        /* camera ray: den >= ((Hmin - 12u D1) winf - 36u D1 w1) / Dinf */
+        double Dinf = 0, winf = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
+        for (int k = 0; k < 3; k++) {
+            double a = fabs(b[k] - comp(o, k)), e = fabs(b[3 + k] - comp(o, k));
+            Dinf = fmax(Dinf, fmax(a, e));
+        }
+        double H = g_hcam[c - g_cert >= 0 && (c - g_cert) % 7 == 0 ? (c - g_cert) / 7 : 0];
+        double dc = ((H - 12 * u * d1) * winf - 36 * u * d1 * w1) / Dinf;
+        if (dc > den) den = dc;
+    }
     if (g_cert_floor_only == 2) return 1e30;
     g_cert_is_floor = den == fl;
     double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));

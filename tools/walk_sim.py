@@ -202,6 +202,15 @@ def main():
         L.walk_sim_cert(cert.ctypes.data, float(np.abs(pos[:, :3]).max()), int(os.environ.get("WALK_CERT_FLOOR", "0")))
         if os.environ.get("WALK_CELLS"):
             L.walk_sim_cells(P(occ.ctypes.data))
+        if os.environ.get("WALK_CAM"):
+            eye = np.asarray(cfg.camera[0], np.float32)
+            hn = np.abs(((v0.astype(np.float64) - eye.astype(np.float64)) * nst).sum(1)) / np.maximum(Et2, 1e-300)
+            hcam = np.full(n, np.inf)
+            hcam[lv] = leaf_reduce(hn, np.minimum)
+            up(hcam, np.minimum)
+            hcam = np.ascontiguousarray(hcam)
+            L.walk_sim_cam.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
+            L.walk_sim_cam(hcam.ctypes.data, *[float(x) for x in eye])
     L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
     L.walk_sim_cull_every(int(os.environ.get("WALK_CULL_EVERY", "0")))
     L.walk_sim_clip(int(os.environ.get("WALK_CLIP", "0")))
