@@ -528,7 +528,7 @@ __device__ __forceinline__ uint32_t h_ru(float x) { return __half_as_ushort(__fl
 // three-level walk from M reads (interior {axis, plane bits}; leaf {3 |
 // (48*count) << 2, byte offset of its first record}), and the certification
 // data: F = 1e-10 / E2 rounded down to a bf16 (+inf for a subtree without a
-// triangle of non-zero extent) with the camera term H (bf16, k_treelet_hcam)
+// triangle of non-zero extent) with the camera term G (f16, k_treelet_hcam)
 // in the same dword, and the normal box divided by E2 (|x| <= 2: |n*_i| <=
 // 2 E2) as its centre c (f16, nearest) and radius r (f16, rounded up, so that
 // the box lies inside [c - r, c + r]).
@@ -579,7 +579,7 @@ __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const 
             }
         }
         // F as a bf16 (the float's high half: truncation, i.e. rounded down for a
-        // positive F); the high half is the camera term H (k_treelet_hcam), 0 until set
+        // positive F); the high half is the camera term G (k_treelet_hcam), 0 until set
         o[20] = __float_as_uint(F) >> 16;
         o[21] = hb[0] | (hb[1] << 16);
         o[22] = hb[2] | (hb[3] << 16);
@@ -650,13 +650,32 @@ __global__ void __launch_bounds__(256) k_node_hcam(const uint32_t* tree, uint32_
         h[i] = fminf(h[2 * (size_t)i + 1], h[2 * (size_t)i + 2]);
     }
 }
-// the bf16 of H (truncated: rounded down) into the high half of treelet M's q5.x
-__global__ void __launch_bounds__(256) k_treelet_hcam(const float* h, uint32_t nnodes, uint32_t* tl)
+// The camera term G of treelet M, into the high half of its q5.x as an f16
+// rounded down (G <= 2 sqrt(3): |n*| <= 2 E_T^2, |v0 - E| <= sqrt(3) Dinf): with D1 and Dinf the L1 and L-inf bounds of
+// |x - E| over the treelet's box (f64, rounded up) and H the subtree's minimum
+// above, a camera ray's |denom| / E_T^2 >= ((H - 14u D1) |w|inf - 38u D1 |w|1) / Dinf
+// >= |w|inf (H - 128u D1) / Dinf = G |w|inf, since |w|1 <= 3 |w|inf (u = 2^-24;
+// the factor 1 - 2^-20 covers the kernel's one rounding of G |w|inf).
+__global__ void __launch_bounds__(256) k_treelet_hcam(const float* h, uint32_t nnodes, double ex, double ey, double ez,
+                                                      uint32_t* tl)
 {
     constexpr uint32_t W = BSP_TREELET_BYTES / 4;
+    const double E[3] = {ex, ey, ez};
     for (size_t m = 1 + (size_t)blockIdx.x * 256u + threadIdx.x; m <= nnodes; m += (size_t)gridDim.x * 256u) {
-        uint32_t* o = tl + W * m + 20;
-        *o = (*o & 0xFFFFu) | (__float_as_uint(h[m - 1]) & 0xFFFF0000u);
+        uint32_t* t = tl + W * m;
+        double D1 = 0.0, Dinf = 0.0;
+        for (int a = 0; a < 3; a++) {
+            const double d = fmax(fabs((double)__uint_as_float(t[a]) - E[a]), fabs((double)__uint_as_float(t[3 + a]) - E[a]));
+            D1 += d;
+            Dinf = fmax(Dinf, d);
+        }
+        D1 *= 1.0 + 0x1p-40;
+        Dinf *= 1.0 + 0x1p-40;
+        const double H = h[m - 1];
+        float G = 0.0f;
+        if (H == INFINITY) G = INFINITY;   // no triangle of non-zero extent: F is +inf too
+        else if (Dinf > 0.0 && H - 128.0 * 0x1p-24 * D1 > 0.0) G = f_rd((H - 128.0 * 0x1p-24 * D1) / Dinf * (1.0 - 0x1p-20));
+        t[20] = (t[20] & 0xFFFFu) | (h_rd(G) << 16);
     }
 }
 int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, const uint4* idx, const uint32_t* ids,
@@ -673,7 +692,8 @@ int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, 
         const uint32_t g = std::min<uint32_t>(16384, (hi - lo + 255) / 256);
         hipLaunchKernelGGL(k_node_hcam, dim3(g), dim3(256), 0, s, tree, nnodes, lo, hi, h);
     }
-    hipLaunchKernelGGL(k_treelet_hcam, dim3(g0), dim3(256), 0, s, h, nnodes, reinterpret_cast<uint32_t*>(blob));
+    hipLaunchKernelGGL(k_treelet_hcam, dim3(g0), dim3(256), 0, s, h, nnodes, (double)eye[0], (double)eye[1], (double)eye[2],
+                       reinterpret_cast<uint32_t*>(blob));
     return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }
 

@@ -75,6 +75,10 @@ __device__ __forceinline__ uint32_t lane_v()
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
+typedef float v2f __attribute__((ext_vector_type(2)));
+#ifndef RT_PK_SLAB
+#define RT_PK_SLAB 0
+#endif
 __device__ __forceinline__ float4 as_f4(v4u q)
 {
     return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
@@ -661,6 +665,12 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // compiler (k_direct's shadow walk culled in the lanes that had been inactive
 // where the mask was computed; tests/test_gpu_cull.py caught it).  The mode
 // is data for the same reason (DevScene cull_k1 / cull_k3 / cull_ko).
+#ifndef RT_AB_CULL_FORMULA
+#define RT_AB_CULL_FORMULA 0
+#endif
+#ifndef RT_AB_CULL_CAM
+#define RT_AB_CULL_CAM 1
+#endif
 __device__ __forceinline__ float h2f(uint32_t bits) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits); }
 __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, const v4u q1, const v4u q5, const f3 o,
                                              const f3 w, const f3 inv, float tmin, float tmax, float& lo, float& hi)
@@ -668,6 +678,15 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
     const float oo[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
     // vectors from the origin to the box's faces; D1 bounds |v0 - o|_1 over the box
     float dl[3], dh[3], D1 = 0.0f;
+#if RT_AB_CULL_FORMULA == 1   // A/B only: the fast margin's formula alone (no certified terms)
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        dl[a] = __uint_as_float(a == 0 ? q0.x : (a == 1 ? q0.y : q0.z)) - oo[a];
+        dh[a] = __uint_as_float(a == 0 ? q0.w : (a == 1 ? q1.x : q1.y)) - oo[a];
+    }
+    const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z)) * S.cull_ko,
+                                    S.bsp_margin);
+#else
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         dl[a] = __uint_as_float(a == 0 ? q0.x : (a == 1 ? q0.y : q0.z)) - oo[a];
@@ -681,26 +700,41 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
     // |w . n*| / E2 >= 2 Dlb over the normal box, stored as centre c and
     // radius r (f16): the box's minimum of |w . x| is |w . c| - |w| . r
     // (fused multiply-adds of f16 and f32 operands: v_fma_mix_f32)
-    const float wc = __builtin_fmaf(w.z, h2f(q5.z & 0xFFFFu), __builtin_fmaf(w.y, h2f(q5.y >> 16), w.x * h2f(q5.y & 0xFFFFu)));
+    // (the first terms as fma(x, y, 0): one v_fma_mix_f32 each, no conversion; only
+    // the sign of a zero product can differ, and |w . c| and |w| . r do not see it)
+    const float wc = __builtin_fmaf(w.z, h2f(q5.z & 0xFFFFu),
+                                    __builtin_fmaf(w.y, h2f(q5.y >> 16), __builtin_fmaf(w.x, h2f(q5.y & 0xFFFFu), 0.0f)));
     const float wr = __builtin_fmaf(rt_absf(w.z), h2f(q5.w >> 16),
-                                    __builtin_fmaf(rt_absf(w.y), h2f(q5.w & 0xFFFFu), rt_absf(w.x) * h2f(q5.z >> 16)));
+                                    __builtin_fmaf(rt_absf(w.y), h2f(q5.w & 0xFFFFu),
+                                                   __builtin_fmaf(rt_absf(w.x), h2f(q5.z >> 16), 0.0f)));
     const float dlb2 = rt_absf(wc) - wr;
     float den = __builtin_fmaxf(__uint_as_float(q5.x << 16), dlb2 - (20.0f * 0x1p-24f) * w1);
-    // a camera ray (its origin is the eye the treelets' camera terms H are for):
-    // |denom| / E_T^2 >= ((H - 14u D1) |w|inf - 38u D1 w1) / Dinf, Dinf >= |x - o|inf
-    // over the box (DESIGN.md section 4 "Certified culling", the camera bound)
+    // a camera ray (its origin is the eye the treelets' camera terms are for):
+    // |denom| / E_T^2 >= G |w|inf, G (f16) precomputed per treelet for the eye
+    // (k_treelet_hcam; DESIGN.md section 4 "Certified culling", the camera bound)
     const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
-    const float Dinf = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(rt_absf(dl[0]), rt_absf(dh[0])),
-                                                       __builtin_fmaxf(rt_absf(dl[1]), rt_absf(dh[1]))),
-                                       __builtin_fmaxf(rt_absf(dl[2]), rt_absf(dh[2])));
     const float winf = __builtin_fmaxf(__builtin_fmaxf(rt_absf(w.x), rt_absf(w.y)), rt_absf(w.z));
-    const float H = __uint_as_float(q5.x & 0xFFFF0000u);
-    const float dcam = ((H - (14.0f * 0x1p-24f) * D1) * winf - (38.0f * 0x1p-24f) * D1 * w1) * __builtin_amdgcn_rcpf(Dinf);
-    den = __builtin_fmaxf(den, cam ? dcam : 0.0f);
+    const float dcam = __builtin_fmaf(winf, h2f(q5.x >> 16), 0.0f);   // G: f16 in the high half
+    if (RT_AB_CULL_CAM) den = __builtin_fmaxf(den, cam ? dcam : 0.0f);
     const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
-    const float m = D1 * (S.cull_k1 * w1 * __builtin_amdgcn_rcpf(den) + S.cull_k3) +
-                    __builtin_fmaxf(mo * S.cull_ko, S.bsp_margin);
+    // (fused: fewer roundings than the proof's constants allow for)
+    const float m = __builtin_fmaf(D1, __builtin_fmaf(S.cull_k1 * w1, __builtin_amdgcn_rcpf(den), S.cull_k3),
+                                   __builtin_fmaxf(mo * S.cull_ko, S.bsp_margin));
+#endif
     float tn = tmin, tf = tmax;
+#if RT_PK_SLAB
+    // the slab pairs as packed f32 (v_pk_add_f32 / v_pk_mul_f32: two lanes' worth
+    // per issue; the same IEEE operations as the scalar form)
+    const v2f mm = {-m, m};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : __builtin_nanf("");
+        const v2f dd = {dl[a], dh[a]};
+        const v2f t = (dd + mm) * ib;
+        tn = __builtin_fmaxf(tn, __builtin_fminf(t.x, t.y));
+        tf = __builtin_fminf(tf, __builtin_fmaxf(t.x, t.y));
+    }
+#else
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : __builtin_nanf("");
@@ -708,13 +742,16 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
         tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
         tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
     }
+#endif
     // a clear gap: the rounding of the slab products cannot close it
     const float e = (rt_absf(tn) + rt_absf(tf)) * S.bsp_cull_gap;
     // the interval the subtree's content can be hit in, widened by the same
     // tolerance (RT_BSP_CLIP; culling off: e = inf or NaN, lo = tmin, hi = tmax)
     lo = __builtin_fmaxf(tmin, tn - e);
     hi = __builtin_fminf(tmax, tf + e);
-    return tn - tf > e;
+    // an empty subtree's content box is +inf / -inf (its slabs are NaN, never a
+    // gap): culled outright, except with culling off (e = inf or NaN)
+    return (tn - tf > e) | (__uint_as_float(q0.x) - __uint_as_float(q0.w) > e);
 }
 
 // The walking half of a BSP trip: node m (level 0), a child (level 1), a

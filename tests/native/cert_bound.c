@@ -117,22 +117,33 @@ static float cert_margin(v3 v0, v3 v1, v3 v2, v3 o, v3 w, float scene, float bmi
         double eta = fabs(dot) - err;
         float H = E2 > 0 ? (eta > 0 ? (float)(eta / E2 * (1.0 - 0x1p-19)) : 0.0f) : INFINITY;
         H = nextafterf(H, 0.0f);
-        uint32_t hb;
-        memcpy(&hb, &H, 4);
-        hb &= 0xFFFF0000u;
-        memcpy(&H, &hb, 4);
-        float Dinf = 0.0f;
-        for (int a = 0; a < 3; a++) Dinf = fmaxf(Dinf, fmaxf(fabsf(bmin[a] - oo[a]), fabsf(bmax[a] - oo[a])));
+        /* the treelet's camera term G (rt_bsp_build.hip k_treelet_hcam): from H (f32),
+         * the box's L1 / L-inf distances to the eye (f64, rounded up), rounded down,
+         * an f16 rounded down as the treelet stores it */
+        double D1e = 0.0, Dinfe = 0.0;
+        for (int a = 0; a < 3; a++) {
+            double d = fmax(fabs((double)bmin[a] - oo[a]), fabs((double)bmax[a] - oo[a]));
+            D1e += d;
+            Dinfe = fmax(Dinfe, d);
+        }
+        D1e *= 1.0 + 0x1p-40;
+        Dinfe *= 1.0 + 0x1p-40;
+        float G = 0.0f;
+        if (H == INFINITY) G = INFINITY;
+        else if (Dinfe > 0.0 && H - 128.0 * 0x1p-24 * D1e > 0.0) {
+            G = (float)((H - 128.0 * 0x1p-24 * D1e) / Dinfe * (1.0 - 0x1p-20));
+            G = nextafterf(G, 0.0f);
+        }
+        G = isinf(G) ? G : (float)h_round(G, -1);   /* f16, rounded down */
         float winf = fmaxf(fmaxf(fabsf(w.x), fabsf(w.y)), fabsf(w.z));
-        float rc = nextafterf(1.0f / Dinf, INFINITY);   /* v_rcp_f32 within 1 ulp: the worse side here */
-        float dcam = ((H - (14.0f * 0x1p-24f) * D1) * winf - (38.0f * 0x1p-24f) * D1 * w1) * rc;
+        float dcam = G * winf;
         if (dcam > den) g_cam_binds++;
         den = fmaxf(den, dcam);
     }
     float mo = fmaxf(fmaxf(fabsf(o.x), fabsf(o.y)), fabsf(o.z));
     /* v_rcp_f32 is within 1 ulp: emulate the worse side */
     float rc = nextafterf(1.0f / den, 0.0f);
-    return D1 * ((36.0f * 0x1p-24f) * w1 * rc + 2.0f * 0x1p-24f) + fmaxf(mo * 0x1p-19f, scene * 0x1p-19f);
+    return fmaf(D1, fmaf((36.0f * 0x1p-24f) * w1, rc, 2.0f * 0x1p-24f), fmaxf(mo * 0x1p-19f, scene * 0x1p-19f));
 }
 
 int main(int argc, char** argv)

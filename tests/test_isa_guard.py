@@ -51,10 +51,11 @@ WHOLE_BUDGET = {
     # round 4: the certified culling margin keeps three per-ray terms of the box
     # test in registers across the trip loop (w1 x 20u, w1 x k1, the origin
     # margin) and the 96-B treelets a sixth load: 104/90 and 64/59 (from 72/67, 44/43);
-    # the camera bound (eye compare, |w|inf, the eye term) 108/93 and 68/58.
+    # the camera bound (eye compare, |w|inf, the eye term) 108/93 and 68/58; its
+    # per-treelet precomputed form 108/93 and 64/56.
     "k_pathILi4ELi0ELb0": (108, 93),    # W9E1, BSP
     "k_pathILi4ELi1ELb0": (80, 77),     # W9E1, BVH
-    "k_pathILi3ELi0ELb0": (68, 58),     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
+    "k_pathILi3ELi0ELb0": (64, 56),     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
 }
 
 

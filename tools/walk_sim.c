@@ -112,14 +112,14 @@ static double cert_margin_c(const double* c, v3 o, v3 d, const float* b)
     double fl = 1e-10 / E2;
     if (g_cert_floor_only || den < fl) den = fl;
     if (g_hcam && o.x == g_eye.x && o.y == g_eye.y && o.z == g_eye.z) {
-        /* camera ray: den >= ((Hmin - 12u D1) winf - 36u D1 w1) / Dinf */
+        /* camera ray: den >= winf (Hmin - 128u D1) / Dinf (rt_bsp_build.hip k_treelet_hcam) */
         double Dinf = 0, winf = fmax(fmax(fabs(d.x), fabs(d.y)), fabs(d.z));
         for (int k = 0; k < 3; k++) {
             double a = fabs(b[k] - comp(o, k)), e = fabs(b[3 + k] - comp(o, k));
             Dinf = fmax(Dinf, fmax(a, e));
         }
         double H = g_hcam[c - g_cert >= 0 && (c - g_cert) % 7 == 0 ? (c - g_cert) / 7 : 0];
-        double dc = ((H - 12 * u * d1) * winf - 36 * u * d1 * w1) / Dinf;
+        double dc = winf * (H - 128 * u * d1) / Dinf;
         if (dc > den) den = dc;
     }
     if (g_cert_floor_only == 2) return 1e30;
