@@ -189,7 +189,8 @@ typedef struct rt_ray_counts {
                                      triangle sequence, by construction */
 #define RT_BSP_CULL_CERTIFIED  1  /* (default) the margin is a proven bound on how far an f32 accept of
                                      intersect_triangle (w7e3.wgsl:286-332) can lie from its triangle's box, from the
-                                     subtree's largest edge and its box of normals: every hit (triangle, distance,
+                                     subtree's largest edge, its box of normals and, for rays that start at the
+                                     uniforms' camera eye, its per-eye plane distance: every hit (triangle, distance,
                                      barycentrics) is bit-identical to RT_BSP_CULL_OFF for every ray; only hitless
                                      work is skipped */
 #define RT_BSP_CULL_FAST       2  /* the margin is 2^-10 of the scene's / the ray origin's coordinate magnitude: not
