@@ -320,8 +320,11 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
         c->waves_per_cu = (int)value;
         return RT_OK;
     case RT_OPT_SHADE_THRESHOLD:
-        if (value < -1 || value > 64)
-            return fail(c, RT_E_INVALID, "shade threshold must be in [0,64] (64 = lockstep), or -1 (the default)");
+        // 0x10000 | hi << 8 | lo: the per-wave choice between lo and hi (BSP walk)
+        if ((value < -1 || value > 64) &&
+            !((value & ~0x1FFFF) == 0 && (value & 0x10000) && (value & 0xFF) <= 64 && ((value >> 8) & 0xFF) <= 64))
+            return fail(c, RT_E_INVALID, "shade threshold must be in [0,64] (64 = lockstep), 0x10000 | hi << 8 | lo "
+                                         "(a per-wave choice, hi and lo in [0,64]), or -1 (the default)");
         c->shade_threshold = (int)value;
         return RT_OK;
     case RT_OPT_SAMPLE_CHUNK:
@@ -965,14 +968,20 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // BVH 2-4 best, 4695 vs 4604 Mrays/s at 8)
     // defaults per walk and shader (profiles/r02/ab_w7e3_shards.txt: W7E3's short
     // Cornell-box rays shade often, and refilling earlier pays there)
-    // The BSP walk of the other modes chooses per wave between 8 and 24 (bit 16:
-    // adaptive, k_path "Shading threshold"): 8 for walk-dominated scenes (config
-    // 3), 24 for test-dominated ones (configs 4 and 5 since subtree culling; fixed
-    // thresholds 12..48 on them: 24 best, profiles/r03/ab_T{hi,lo}_c{4,5}.txt).
+    // The BSP walk of the other modes chooses per wave between two thresholds (bit
+    // 16: adaptive, k_path "Shading threshold"), the lower for walk-dominated waves,
+    // the higher for test-dominated ones.  With the fast margin 8 and 24 (configs 4
+    // and 5 test-dominated since subtree culling; fixed thresholds 12..48 on them: 24
+    // best, profiles/r03/ab_T{hi,lo}_c{4,5}.txt).  The certified walk visits more
+    // nodes and its rays take more trips, so finished lanes wait longer for the last
+    // ones: 16 and 32 (profiles/r04/sweep_T.txt: config 3 fixed 16 +1.9 % over 8,
+    // config 4 16..24 +3 %, config 5 32 +1.1 %).
+    const uint32_t adaptive = c->bsp_cull == RT_BSP_CULL_CERTIFIED ? (1u << 16) | (32u << 8) | 16u
+                                                                   : (1u << 16) | (24u << 8) | 8u;
     L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold
                                    : trav == RT_TRAVERSE_BVH ? 4
                                    : mode == RT_MODE_W7E3    ? 24
-                                                             : (1u << 16) | (24u << 8) | 8u);
+                                                             : adaptive);
     L.reserved0 = 0;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));

@@ -199,7 +199,8 @@ def main():
     ap.add_argument("--ntris", type=int, default=None)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--shade-threshold", type=int, default=None)
+    ap.add_argument("--shade-threshold", type=lambda x: int(x, 0), default=None,
+                    help="RT_OPT_SHADE_THRESHOLD: 0..64, or 0x10000 | hi << 8 | lo (a per-wave choice)")
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)

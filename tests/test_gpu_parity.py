@@ -172,7 +172,7 @@ def test_shade_threshold_is_scheduling_only(rt, gpu, depth):
     region = (600, 300, 96, 64)
     frames = {}
     try:
-        for t in (-1, 8, 24, 32, 0, 64):
+        for t in (-1, 8, 24, 32, 0, 64, 0x10000 | (32 << 8) | 12):
             s.ctx.set_option(rt._ffi.RT_OPT_SHADE_THRESHOLD, t)
             frames[t] = s.render_gpu("W9E1", cam, 1280, 720, region, 0, 3)
     finally:
