@@ -162,17 +162,18 @@ def test_bunny_w9e1_bvh_region(rt, gpu):
 
 @pytest.mark.parametrize("depth", [20, 9])
 def test_shade_threshold_is_scheduling_only(rt, gpu, depth):
-    # The shading threshold only schedules: every setting -- fixed 8, 24 or 32,
-    # lockstep (0 and 64), and the default per-wave choice between T_lo 8 and
-    # T_hi 24 from the wave's share of lanes inside a leaf (k_path) -- renders the
-    # same bits.  Depth 9 makes a test-dominated walk (~300 triangles per leaf: the
-    # share is high and the waves choose 24), depth 20 a walk-dominated one (8).
+    # The shading threshold only schedules: every setting -- fixed 8, 16, 24 or 32,
+    # lockstep (0 and 64), an explicit per-wave pair, and the default per-wave choice
+    # from the wave's share of lanes inside a leaf (k_path; T_lo 16 / T_hi 32 with
+    # the default certified culling, 8 / 24 with the fast margin) -- renders the same
+    # bits.  Depth 9 makes a test-dominated walk (~300 triangles per leaf: the share
+    # is high and the waves choose T_hi), depth 20 a walk-dominated one (T_lo).
     s = Scene(rt, rt.Mesh.synth_soup(150_000), "BSP", oracle_accel_from_product=True, bsp_depth=depth)
     cam = ((0.0, 0.0, 3.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 1.5)
     region = (600, 300, 96, 64)
     frames = {}
     try:
-        for t in (-1, 8, 24, 32, 0, 64, 0x10000 | (32 << 8) | 12):
+        for t in (-1, 8, 16, 24, 32, 0, 64, 0x10000 | (32 << 8) | 12):
             s.ctx.set_option(rt._ffi.RT_OPT_SHADE_THRESHOLD, t)
             frames[t] = s.render_gpu("W9E1", cam, 1280, 720, region, 0, 3)
     finally:
