@@ -640,7 +640,8 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // with D1 >= |v0 - o|_1 for every point v0 of the box, w1 = |w|_1, F = 1e-10 /
 // E2 and 2 Dlb a lower bound of |w . n*| / E2 over the subtree's normals from
 // the treelet's normal box (q5: centre and radius of n* / E2); for a camera ray
-// also a bound from how far the eye is from its triangles' planes (q5's H).  Certified mode (k1 = 36u, k3 = 2u, ko and
+// also G |w|inf, G precomputed per treelet from how far the eye is from its
+// triangles' planes (q5.x's high half, k_treelet_hcam).  Certified mode (k1 = 36u, k3 = 2u, ko and
 // dscene 2^-19 of the magnitudes): m bounds the L-inf distance from the box of
 // every point o + dist*w where intersect_triangle (w7e3.wgsl:286-332) can
 // accept one of the subtree's triangles -- its f32 rounding, including
@@ -665,6 +666,9 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // compiler (k_direct's shadow walk culled in the lanes that had been inactive
 // where the mask was computed; tests/test_gpu_cull.py caught it).  The mode
 // is data for the same reason (DevScene cull_k1 / cull_k3 / cull_ko).
+#ifndef RT_AB_EXTRA_LIVE
+#define RT_AB_EXTRA_LIVE 0
+#endif
 #ifndef RT_AB_CULL_FORMULA
 #define RT_AB_CULL_FORMULA 0
 #endif
@@ -833,8 +837,23 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
             c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
     }
     bool done = false, pop = false;
+#if RT_AB_EXTRA_LIVE
+    // A/B probe only (DESIGN.md section 4 "Round 4"): RT_AB_EXTRA_LIVE more values
+    // live across both halves of the trip, the registers a wave-cooperative leaf
+    // test needs for a helper lane's copy of its owner's ray (o, w, tmin, tmax)
+    float xl[RT_AB_EXTRA_LIVE];
+#pragma unroll
+    for (int i = 0; i < RT_AB_EXTRA_LIVE; i++) {
+        xl[i] = i < 3 ? comp(o, i) : i < 6 ? comp(d, i - 3) : i == 6 ? t.tmin : t.tmax;
+        asm volatile("" : "+v"(xl[i]));
+    }
+#endif
     if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg);
     else bsp_walk<COUNT>(S, stk, q0, q1, q2, q3, q4, q5, o, d, inv, t, c, pop);
+#if RT_AB_EXTRA_LIVE
+#pragma unroll
+    for (int i = 0; i < RT_AB_EXTRA_LIVE; i++) asm volatile("" : : "v"(xl[i]));
+#endif
     if (pop) done = bsp_pop(stk, t);
     return done;
 }
