@@ -201,6 +201,10 @@ struct Pix {
     uint32_t x, y, out;
     bool valid;
 };
+// A/B knob: the tile rows' rotation is (ty * RT_TILE_ROT) mod 8 (1: tiling.tile_of_seq)
+#ifndef RT_TILE_ROT
+#define RT_TILE_ROT 1u
+#endif
 __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint32_t lane)
 {
     Pix p;
@@ -219,7 +223,7 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
         // columns tx = r + ty (mod nranks) when nranks divides 8 and tiles_x
         // (1080p: 240 tile columns); frames under 8 tiles wide are not rotated
         uint32_t t = work * L.nranks + L.rank;
-        uint32_t ty = t / tiles_x, tx = t - ty * tiles_x + (tiles_x >= 8u ? (ty & 7u) : 0u);
+        uint32_t ty = t / tiles_x, tx = t - ty * tiles_x + (tiles_x >= 8u ? ((ty * RT_TILE_ROT) & 7u) : 0u);
         tx = tx >= tiles_x ? tx - tiles_x : tx;
         p.x = tx * 8u + lx;
         p.y = ty * 8u + ly;
@@ -234,7 +238,7 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
 __device__ __forceinline__ uint32_t pixel_out(const DevLaunch& L, uint32_t x, uint32_t y)
 {
     if (L.tileset == 0) return (y - L.y0) * L.w + (x - L.x0);
-    const uint32_t ty = y >> 3, tx = x >> 3, r = L.tiles_x >= 8u ? (ty & 7u) : 0u;
+    const uint32_t ty = y >> 3, tx = x >> 3, r = L.tiles_x >= 8u ? ((ty * RT_TILE_ROT) & 7u) : 0u;
     const uint32_t t = ty * L.tiles_x + (tx >= r ? tx - r : tx + L.tiles_x - r);   // map_pixel's s
     return (t - L.rank) / L.nranks * 64u + ((y & 7u) << 3) + (x & 7u);
 }
@@ -2561,7 +2565,7 @@ __global__ void __launch_bounds__(256) k_unpack(uint32_t W, uint32_t H, uint32_t
         // t: the sequence position (map_pixel: rows rotated by their index mod 8)
         const uint32_t t = (uint32_t)(g >> 6), lane = (uint32_t)(g & 63u);
         const uint32_t ty = t / tiles_x;
-        uint32_t tx = t - ty * tiles_x + (tiles_x >= 8u ? (ty & 7u) : 0u);
+        uint32_t tx = t - ty * tiles_x + (tiles_x >= 8u ? ((ty * RT_TILE_ROT) & 7u) : 0u);
         tx = tx >= tiles_x ? tx - tiles_x : tx;
         const uint32_t x = tx * 8u + (lane & 7u), y = ty * 8u + (lane >> 3);
         if (x >= W || y >= H) continue;
