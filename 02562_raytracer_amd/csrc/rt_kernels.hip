@@ -670,6 +670,9 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // compiler (k_direct's shadow walk culled in the lanes that had been inactive
 // where the mask was computed; tests/test_gpu_cull.py caught it).  The mode
 // is data for the same reason (DevScene cull_k1 / cull_k3 / cull_ko).
+#ifndef RT_AB_NO_CONE
+#define RT_AB_NO_CONE 0
+#endif
 #ifndef RT_AB_EXTRA_LIVE
 #define RT_AB_EXTRA_LIVE 0
 #endif
@@ -716,7 +719,12 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
                                     __builtin_fmaf(rt_absf(w.y), h2f(q5.w & 0xFFFFu),
                                                    __builtin_fmaf(rt_absf(w.x), h2f(q5.z >> 16), 0.0f)));
     const float dlb2 = rt_absf(wc) - wr;
+#if RT_AB_NO_CONE   // A/B only: without the normal-box term
+    float den = __uint_as_float(q5.x << 16);
+    (void)dlb2;
+#else
     float den = __builtin_fmaxf(__uint_as_float(q5.x << 16), dlb2 - (20.0f * 0x1p-24f) * w1);
+#endif
     // a camera ray (its origin is the eye the treelets' camera terms are for):
     // |denom| / E_T^2 >= G |w|inf, G (f16) precomputed per treelet for the eye
     // (k_treelet_hcam; DESIGN.md section 4 "Certified culling", the camera bound)
