@@ -683,60 +683,55 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 #define RT_AB_CULL_CAM 1
 #endif
 __device__ __forceinline__ float h2f(uint32_t bits) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits); }
+// CERT false: the fast margin's formula alone, m = max(|o|inf ko, dscene), for a
+// context whose culling is not RT_BSP_CULL_CERTIFIED (the host picks k_path's
+// instantiation, so the fast and off modes do not pay for the certified terms;
+// off keeps the +inf gap factor either way).  The generic (CERT true) form
+// evaluates every mode from its data constants.
+template <bool CERT = true>
 __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, const v4u q1, const v4u q5, const f3 o,
                                              const f3 w, const f3 inv, float tmin, float tmax, float& lo, float& hi)
 {
+    constexpr bool FULL = CERT && RT_AB_CULL_FORMULA != 1;   // (RT_AB_CULL_FORMULA 1: A/B only)
     const float oo[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
     // vectors from the origin to the box's faces; D1 bounds |v0 - o|_1 over the box
     float dl[3], dh[3], D1 = 0.0f;
-#if RT_AB_CULL_FORMULA == 1   // A/B only: the fast margin's formula alone (no certified terms)
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         dl[a] = __uint_as_float(a == 0 ? q0.x : (a == 1 ? q0.y : q0.z)) - oo[a];
         dh[a] = __uint_as_float(a == 0 ? q0.w : (a == 1 ? q1.x : q1.y)) - oo[a];
+        if (FULL) D1 += __builtin_fmaxf(rt_absf(dl[a]), rt_absf(dh[a]));
     }
-    const float m = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z)) * S.cull_ko,
-                                    S.bsp_margin);
-#else
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        dl[a] = __uint_as_float(a == 0 ? q0.x : (a == 1 ? q0.y : q0.z)) - oo[a];
-        dh[a] = __uint_as_float(a == 0 ? q0.w : (a == 1 ? q1.x : q1.y)) - oo[a];
-        D1 += __builtin_fmaxf(rt_absf(dl[a]), rt_absf(dh[a]));
-    }
-    // (the compiler keeps w1's products and the origin term in registers across
-    // the trip loop; recomputing them every trip, through an opaque asm, was
-    // 2.5 % slower: profiles/r04/ab_opq.txt)
-    const float w1 = rt_absf(w.x) + rt_absf(w.y) + rt_absf(w.z);
-    // |w . n*| / E2 >= 2 Dlb over the normal box, stored as centre c and
-    // radius r (f16): the box's minimum of |w . x| is |w . c| - |w| . r
-    // (fused multiply-adds of f16 and f32 operands: v_fma_mix_f32)
-    // (the first terms as fma(x, y, 0): one v_fma_mix_f32 each, no conversion; only
-    // the sign of a zero product can differ, and |w . c| and |w| . r do not see it)
-    const float wc = __builtin_fmaf(w.z, h2f(q5.z & 0xFFFFu),
-                                    __builtin_fmaf(w.y, h2f(q5.y >> 16), __builtin_fmaf(w.x, h2f(q5.y & 0xFFFFu), 0.0f)));
-    const float wr = __builtin_fmaf(rt_absf(w.z), h2f(q5.w >> 16),
-                                    __builtin_fmaf(rt_absf(w.y), h2f(q5.w & 0xFFFFu),
-                                                   __builtin_fmaf(rt_absf(w.x), h2f(q5.z >> 16), 0.0f)));
-    const float dlb2 = rt_absf(wc) - wr;
-#if RT_AB_NO_CONE   // A/B only: without the normal-box term
-    float den = __uint_as_float(q5.x << 16);
-    (void)dlb2;
-#else
-    float den = __builtin_fmaxf(__uint_as_float(q5.x << 16), dlb2 - (20.0f * 0x1p-24f) * w1);
-#endif
-    // a camera ray (its origin is the eye the treelets' camera terms are for):
-    // |denom| / E_T^2 >= G |w|inf, G (f16) precomputed per treelet for the eye
-    // (k_treelet_hcam; DESIGN.md section 4 "Certified culling", the camera bound)
-    const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
-    const float winf = __builtin_fmaxf(__builtin_fmaxf(rt_absf(w.x), rt_absf(w.y)), rt_absf(w.z));
-    const float dcam = __builtin_fmaf(winf, h2f(q5.x >> 16), 0.0f);   // G: f16 in the high half
-    if (RT_AB_CULL_CAM) den = __builtin_fmaxf(den, cam ? dcam : 0.0f);
     const float mo = __builtin_fmaxf(__builtin_fmaxf(rt_absf(o.x), rt_absf(o.y)), rt_absf(o.z));
-    // (fused: fewer roundings than the proof's constants allow for)
-    const float m = __builtin_fmaf(D1, __builtin_fmaf(S.cull_k1 * w1, __builtin_amdgcn_rcpf(den), S.cull_k3),
-                                   __builtin_fmaxf(mo * S.cull_ko, S.bsp_margin));
-#endif
+    float m = __builtin_fmaxf(mo * S.cull_ko, S.bsp_margin);
+    if constexpr (FULL) {
+        // (the compiler keeps w1's products and the origin term in registers across
+        // the trip loop; recomputing them every trip, through an opaque asm, was
+        // 2.5 % slower: profiles/r04/ab_opq.txt)
+        const float w1 = rt_absf(w.x) + rt_absf(w.y) + rt_absf(w.z);
+        // |w . n*| / E2 >= 2 Dlb over the normal box, stored as centre c and
+        // radius r (f16): the box's minimum of |w . x| is |w . c| - |w| . r
+        // (fused multiply-adds of f16 and f32 operands: v_fma_mix_f32)
+        // (the first terms as fma(x, y, 0): one v_fma_mix_f32 each, no conversion; only
+        // the sign of a zero product can differ, and |w . c| and |w| . r do not see it)
+        const float wc = __builtin_fmaf(w.z, h2f(q5.z & 0xFFFFu),
+                                        __builtin_fmaf(w.y, h2f(q5.y >> 16), __builtin_fmaf(w.x, h2f(q5.y & 0xFFFFu), 0.0f)));
+        const float wr = __builtin_fmaf(rt_absf(w.z), h2f(q5.w >> 16),
+                                        __builtin_fmaf(rt_absf(w.y), h2f(q5.w & 0xFFFFu),
+                                                       __builtin_fmaf(rt_absf(w.x), h2f(q5.z >> 16), 0.0f)));
+        const float dlb2 = rt_absf(wc) - wr;
+        float den = __uint_as_float(q5.x << 16);
+        if (!RT_AB_NO_CONE) den = __builtin_fmaxf(den, dlb2 - (20.0f * 0x1p-24f) * w1);   // (A/B knob: without it)
+        // a camera ray (its origin is the eye the treelets' camera terms are for):
+        // |denom| / E_T^2 >= G |w|inf, G (f16) precomputed per treelet for the eye
+        // (k_treelet_hcam; DESIGN.md section 4 "Certified culling", the camera bound)
+        const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
+        const float winf = __builtin_fmaxf(__builtin_fmaxf(rt_absf(w.x), rt_absf(w.y)), rt_absf(w.z));
+        const float dcam = __builtin_fmaf(winf, h2f(q5.x >> 16), 0.0f);   // G: f16 in the high half
+        if (RT_AB_CULL_CAM) den = __builtin_fmaxf(den, cam ? dcam : 0.0f);
+        // (fused: fewer roundings than the proof's constants allow for)
+        m = __builtin_fmaf(D1, __builtin_fmaf(S.cull_k1 * w1, __builtin_amdgcn_rcpf(den), S.cull_k3), m);
+    }
     float tn = tmin, tf = tmax;
 #if RT_PK_SLAB
     // the slab pairs as packed f32 (v_pk_add_f32 / v_pk_mul_f32: two lanes' worth
@@ -777,7 +772,7 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
 // trip); an empty leaf, or a subtree culled by its content box, sets pop.
 // (Testing the first record of a leaf in the trip that reaches it -- one more
 // round trip -- was slower: config 4 -3.7 %, config 5 -11 %, profiles/r02/ab_et1.txt.)
-template <bool COUNT>
+template <bool COUNT, bool CERT = true>
 __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4u q0, const v4u q1, const v4u q2,
                                          const v4u q3, const v4u q4, const v4u q5, const f3 o, const f3 d, const f3 inv,
                                          Trav& t, Counters& c, bool& pop)
@@ -786,7 +781,7 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
     float lo = t.tmin, hi = t.tmax;   // the decisions' interval
     if (RT_BSP_CULL) {
         float blo, bhi;
-        if (bsp_box_miss(S, q0, q1, q5, o, d, inv, t.tmin, t.tmax, blo, bhi)) {
+        if (bsp_box_miss<CERT>(S, q0, q1, q5, o, d, inv, t.tmin, t.tmax, blo, bhi)) {
             if (COUNT) c.v[C_CULLS]++;
             pop = true;
             return false;
@@ -823,7 +818,7 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
     return leaf & !pop;
 }
 
-template <bool COUNT, bool CULL, class LOG>
+template <bool COUNT, bool CULL, class LOG, bool CERT = true>
 __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                              bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
@@ -861,7 +856,7 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     }
 #endif
     if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg);
-    else bsp_walk<COUNT>(S, stk, q0, q1, q2, q3, q4, q5, o, d, inv, t, c, pop);
+    else bsp_walk<COUNT, CERT>(S, stk, q0, q1, q2, q3, q4, q5, o, d, inv, t, c, pop);
 #if RT_AB_EXTRA_LIVE
 #pragma unroll
     for (int i = 0; i < RT_AB_EXTRA_LIVE; i++) asm volatile("" : : "v"(xl[i]));
@@ -869,12 +864,12 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     if (pop) done = bsp_pop(stk, t);
     return done;
 }
-template <bool COUNT, bool CULL = false>
+template <bool COUNT, bool CULL = false, bool CERT = true>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
 {
     NoLog lg;
-    return bsp_step_log<COUNT, CULL>(S, stk, o, d, inv, anyhit, t, c, lg);
+    return bsp_step_log<COUNT, CULL, NoLog, CERT>(S, stk, o, d, inv, anyhit, t, c, lg);
 }
 
 // RN(1/denom) per axis (denom as bsp.wgsl:63): the approximate interior-node
@@ -1126,13 +1121,13 @@ __device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float
     if (TRAV == RT_TRAVERSE_BVH) bvh_init(t, tmin, tmax);
     else trav_init(t, tmin, tmax);
 }
-template <int TRAV, bool COUNT, bool CULL = false>
+template <int TRAV, bool COUNT, bool CULL = false, bool CERT = true>
 __device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const BvhDeep& dp, const f3 o, const f3 d,
                                           const f3 inv, bool anyhit, Trav& t, Counters& c)
 {
     if (TRAV == RT_TRAVERSE_BVH)
         return bvh_step<COUNT, CULL>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv, anyhit, t, c);
-    return bsp_step<COUNT, CULL>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
+    return bsp_step<COUNT, CULL, CERT>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
 }
 
 // Whole traversal of one ray (used by the primary-ray kernel).
@@ -1474,7 +1469,10 @@ __device__ __forceinline__ bool w8_ball_shade(const W8Ball& b, f3& ro, f3& rd, f
 // pressure enough to spill inside the traversal loop.
 constexpr int MODE_W9E1_TRANSPARENT = 100 + RT_MODE_W9E1;
 
-template <int MODE, int TRAV, bool COUNT>
+// CERT: the BSP walk's margin formula (bsp_box_miss): true, the generic form every
+// culling mode runs correctly with; false, the fast margin's alone (launch_path
+// picks it for W9E1 when the context's culling is not certified)
+template <int MODE, int TRAV, bool COUNT, bool CERT = true>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     TRAV == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : MODE == RT_MODE_W7E3 ? RT_W7E3_WAVES_PER_EU : RT_PATH_WAVES_PER_EU,
     8)))
@@ -1614,7 +1612,7 @@ k_path(DevScene S, DevLaunch L)
             }
             const bool go = st == ST_TRACE;
             if (go) {
-                if (trav_step<TRAV, COUNT, W9E3>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                if (trav_step<TRAV, COUNT, W9E3, CERT>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }
             // further steps before the next check: the check (two ballots, a
             // popcount, the compares) is SALU work, and the SALU is a per-CU
@@ -1622,7 +1620,7 @@ k_path(DevScene S, DevLaunch L)
 #pragma unroll
             for (int k = 1; k < (COUNT ? 1 : TRAV == RT_TRAVERSE_BVH ? RT_BVH_TRIPS_PER_CHECK : RT_TRIPS_PER_CHECK); ++k) {
                 if (st == ST_TRACE) {
-                    if (trav_step<TRAV, COUNT, W9E3>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                    if (trav_step<TRAV, COUNT, W9E3, CERT>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
                 }
             }
         }
@@ -2699,6 +2697,15 @@ size_t bvh_deep_bytes(int num_cus, int waves_per_cu)
 template <int MODE, int TRAV, bool COUNT>
 static void launch_path(const DevScene& s, const DevLaunch& l, int grid, size_t lds, hipStream_t st)
 {
+    // W9E1's BSP walk (configs 3-5) has a fast-margin instantiation: a context whose
+    // culling is not certified (cull_k1 = 0: fast, or off with its +inf gap) skips the
+    // certified terms (round 3's trip).  The other modes run the generic formula.
+    if constexpr (MODE == RT_MODE_W9E1 && TRAV == RT_TRAVERSE_BSP) {
+        if (s.cull_k1 == 0.0f) {
+            hipLaunchKernelGGL((k_path<MODE, TRAV, COUNT, false>), dim3(grid), dim3(256), lds, st, s, l);
+            return;
+        }
+    }
     hipLaunchKernelGGL((k_path<MODE, TRAV, COUNT>), dim3(grid), dim3(256), lds, st, s, l);
 }
 template <int MODE, int TRAV, bool COUNT>

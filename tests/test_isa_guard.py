@@ -19,9 +19,10 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 BUDGET = {
     # W9E1, BSP: the bench kernel, eight traversal steps per trip
     # (RT_TRIPS_PER_CHECK); none of them spills
-    "k_pathILi4ELi0ELb0": 0,
-    "k_pathILi4ELi1ELb0": 0,   # W9E1, BVH at 8 waves/SIMD (4 before the round-2 spill cuts)
-    "k_pathILi3ELi0ELb0": 0,   # W7E3, BSP at 7 waves/SIMD
+    "k_pathILi4ELi0ELb0ELb1": 0,
+    "k_pathILi4ELi0ELb0ELb0": 0,   # W9E1, BSP, the fast-margin instantiation
+    "k_pathILi4ELi1ELb0ELb1": 0,   # W9E1, BVH at 8 waves/SIMD (4 before the round-2 spill cuts)
+    "k_pathILi3ELi0ELb0ELb1": 0,   # W7E3, BSP at 7 waves/SIMD
 }
 
 
@@ -53,9 +54,10 @@ WHOLE_BUDGET = {
     # margin) and the 96-B treelets a sixth load: 104/90 and 64/59 (from 72/67, 44/43);
     # the camera bound (eye compare, |w|inf, the eye term) 108/93 and 68/58; its
     # per-treelet precomputed form 108/93 and 64/56.
-    "k_pathILi4ELi0ELb0": (108, 93),    # W9E1, BSP
-    "k_pathILi4ELi1ELb0": (80, 77),     # W9E1, BVH
-    "k_pathILi3ELi0ELb0": (64, 56),     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
+    "k_pathILi4ELi0ELb0ELb1": (108, 93),    # W9E1, BSP
+    "k_pathILi4ELi0ELb0ELb0": (88, 99),     # W9E1, BSP, the fast-margin instantiation
+    "k_pathILi4ELi1ELb0ELb1": (80, 77),     # W9E1, BVH
+    "k_pathILi3ELi0ELb0ELb1": (64, 56),     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
 }
 
 

@@ -20,6 +20,6 @@ def loop_stats(path, ksub):
 
 
 if __name__ == "__main__":
-    for k in sys.argv[2:] or ["k_pathILi4ELi0ELb0"]:
+    for k in sys.argv[2:] or ["k_pathILi4ELi0ELb0ELb1"]:
         t = loop_stats(sys.argv[1], k)
         print(k, sum(t.values()), dict(sorted(t.items(), key=lambda x: -x[1])))

@@ -23,5 +23,5 @@ def trip_loop_scratch(path, ksub):
 
 
 if __name__ == "__main__":
-    for k in sys.argv[2:] or ["k_pathILi4ELi0ELb0", "k_pathILi4ELi1ELb0"]:
+    for k in sys.argv[2:] or ["k_pathILi4ELi0ELb0ELb1", "k_pathILi4ELi1ELb0ELb1"]:
         print(k, trip_loop_scratch(sys.argv[1], k))
