@@ -1,6 +1,8 @@
 #!/bin/bash
 # Same-box comparison of the round-3 tree (abr03/, built from 5037b61) with this
 # tree on config 3: usage tools/ab_r03.sh <tag>
+# (recreate abr03/: git worktree add /tmp/r03 5037b61, make -C /tmp/r03/02562_raytracer_amd,
+#  then copy its 02562_raytracer_amd/, bench.py, oracle/ and tools/ into abr03/; git-ignored)
 set -u
 export TMPDIR=/tmp
 O=$PWD/gpurun_out/$1; mkdir -p $O
