@@ -1,12 +1,13 @@
 """Subtree culling at the BASELINE spp of the 8-GPU workloads (DESIGN.md section 4
 "Subtree culling"): the whole config-4 frame at 256 spp and the whole config-5
-frame at 1024 spp, rendered with RT_OPT_BSP_CULL 1 (culled, clipped walk) and
-0 (every node of bsp.wgsl's walk), compared bit for bit: every pixel's
-accumulation, the primary-hit ids and the ray counts.  Too long for the GPU
+frame at 1024 spp (and config 3's at 256), rendered with RT_OPT_BSP_CULL 1
+(certified margin, the default), 2 (fast margin) and 0 (every node of bsp.wgsl's
+walk), compared bit for bit: every pixel's accumulation, the primary-hit ids and
+the ray counts.  Too long for the GPU
 suite (the unculled config-5 frame takes about a minute); run once per kernel
 change, its output committed under profiles/.
 
-  python tools/cull_stress.py [configs, default 4,5]
+  python tools/cull_stress.py [configs, default 3,4,5]
 """
 import importlib
 import os
@@ -38,7 +39,7 @@ def frame(rt, ctx, wl, cull):
 def main():
     rt = importlib.import_module("02562_raytracer_amd")
     wls = importlib.import_module("02562_raytracer_amd.configs").WORKLOADS
-    cfgs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "4,5").split(",")]
+    cfgs = [int(x) for x in (sys.argv[1] if len(sys.argv) > 1 else "3,4,5").split(",")]
     bad_total = 0
     for n in cfgs:
         wl = wls[n]
@@ -49,20 +50,23 @@ def main():
             ctx.upload_bsp(mesh.bsp_tree())
             ctx.set_environment(wl.env)
             ctx.set_uniforms(rt.make_uniform(*wl.camera, wl.width, wl.height))
-            on = frame(rt, ctx, wl, 1)
-            print(f"config {n}: culled frame {on[3]:.1f} s", flush=True)
-            off = frame(rt, ctx, wl, 0)
-            print(f"config {n}: unculled frame {off[3]:.1f} s", flush=True)
+            frames = {}
+            for cull, name in ((1, "certified"), (2, "fast"), (0, "unculled")):
+                frames[name] = frame(rt, ctx, wl, cull)
+                print(f"config {n}: {name} frame {frames[name][3]:.1f} s", flush=True)
         finally:
             ctx.close()
-        px = int((on[0] != off[0]).any(axis=2).sum())
-        idm = int((on[1] != off[1]).sum())
-        cnt = {k: (on[2][k], off[2][k]) for k in ("samples", "primary", "shadow", "bounce")}
-        same = all(a == b for a, b in cnt.values())
-        rays = sum(on[2][k] for k in ("primary", "shadow", "bounce"))
-        print(f"config {n}: {wl.width}x{wl.height} x {wl.spp} spp, {rays} rays: {px} pixels' accumulation differ, "
-              f"{idm} primary ids differ, ray counts {'equal' if same else cnt}", flush=True)
-        bad_total += px + idm + (0 if same else 1)
+        off = frames["unculled"]
+        for name in ("certified", "fast"):
+            on = frames[name]
+            px = int((on[0] != off[0]).any(axis=2).sum())
+            idm = int((on[1] != off[1]).sum())
+            cnt = {k: (on[2][k], off[2][k]) for k in ("samples", "primary", "shadow", "bounce")}
+            same = all(a == b for a, b in cnt.values())
+            rays = sum(on[2][k] for k in ("primary", "shadow", "bounce"))
+            print(f"config {n}, {name}: {wl.width}x{wl.height} x {wl.spp} spp, {rays} rays: {px} pixels' accumulation "
+                  f"differ, {idm} primary ids differ, ray counts {'equal' if same else cnt}", flush=True)
+            bad_total += px + idm + (0 if same else 1)
     sys.exit(1 if bad_total else 0)
 
 
