@@ -670,6 +670,9 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // compiler (k_direct's shadow walk culled in the lanes that had been inactive
 // where the mask was computed; tests/test_gpu_cull.py caught it).  The mode
 // is data for the same reason (DevScene cull_k1 / cull_k3 / cull_ko).
+#ifndef RT_SHADE_PRIO
+#define RT_SHADE_PRIO 0
+#endif
 #ifndef RT_AB_NO_CONE
 #define RT_AB_NO_CONE 0
 #endif
@@ -1634,6 +1637,9 @@ k_path(DevScene S, DevLaunch L)
             tstamp = now;
         }
         {
+        // (A/B: RT_SHADE_PRIO raises the wave's issue priority for its shading and refill
+        // phase, so lanes are refilled sooner while the other waves trace)
+        if (RT_SHADE_PRIO) __builtin_amdgcn_s_setprio(RT_SHADE_PRIO);
         // the shading and refill phases read the kernel arguments afresh (kreload)
         const DevScene& Sk = kreload<DevScene>(KARG_S);
         const DevLaunch& Lk = kreload<DevLaunch>(KARG_L);
@@ -1964,6 +1970,7 @@ k_path(DevScene S, DevLaunch L)
             if (lane == 0) cnt.v[C_SHADE_CYC64] += (uint32_t)((now - tstamp) >> 6);
             tstamp = now;
         }
+        if (RT_SHADE_PRIO) __builtin_amdgcn_s_setprio(0);
         if (__ballot(st != ST_IDLE) == 0) break;
     }
     flush_counters(cnt, L.counters, COUNT);
