@@ -144,6 +144,7 @@ SIGNATURES = {
     "rt_build_bvh_device": (C.c_int, [vp, C.c_uint32, C.POINTER(BvhBuildTimes)]),
     "rt_build_bsp_device": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(BspBuildTimes)]),
     "rt_download_bsp": (C.c_int, [vp, u32p, f32p, C.c_uint32, u32p, C.c_uint32, f32p, u32p, u32p]),
+    "rt_download_bsp_treelets": (C.c_int, [vp, vp, C.c_uint64, C.POINTER(C.c_uint64)]),
     "rt_download_bvh": (C.c_int, [vp, C.POINTER(GpuNode), C.c_uint32, u32p, C.c_uint32, u32p, u32p]),
     "rt_upload_mesh": (C.c_int, [vp, f32p, f32p, C.c_uint32, u32p, C.c_uint32, C.POINTER(Material), C.c_uint32,
                                  u32p, C.c_uint32]),

@@ -299,6 +299,15 @@ class Context:
                                           aabb.ctypes.data_as(F.f32p), C.byref(nn), C.byref(ni)))
         return tree[:nn.value], planes[:nn.value], ids[:ni.value], aabb
 
+    def download_bsp_treelets(self):
+        """The BSP walk's 96-B treelets as u32[nnodes + 1, 24] (rt_download_bsp_treelets;
+        diagnostics: the certified culling's per-subtree data)."""
+        nb = C.c_uint64()
+        self._chk(F.lib().rt_download_bsp_treelets(self._h, None, 0, C.byref(nb)))
+        out = np.zeros(nb.value // 4, np.uint32)
+        self._chk(F.lib().rt_download_bsp_treelets(self._h, out.ctypes.data_as(C.c_void_p), nb.value, C.byref(nb)))
+        return out.reshape(-1, 24)
+
     def download_bvh(self):
         """(nodes[n,8] u32 view of GpuNode, tri_ids[k] u32) of this context's BVH."""
         nn, ni = C.c_uint32(), C.c_uint32()

@@ -750,6 +750,22 @@ int rt_download_bsp(rt_ctx* c, uint32_t* tree, float* planes, uint32_t cap_nodes
     return RT_OK;
 }
 
+static int ensure_hcam(rt_ctx* c);
+int rt_download_bsp_treelets(rt_ctx* c, void* dst, uint64_t cap_bytes, uint64_t* bytes)
+{
+    if (!c) return RT_E_INVALID;
+    if (!c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_download_bsp_treelets: no BSP on the context");
+    const uint64_t n = ((uint64_t)c->bsp_nnodes + 1) * rtk::BSP_TREELET_BYTES;
+    if (bytes) *bytes = n;
+    if (!dst) return RT_OK;
+    if (cap_bytes < n) return fail(c, RT_E_INVALID, "rt_download_bsp_treelets: buffer too small");
+    if (int r = ensure_hcam(c)) return r;
+    if (int r = set_dev(c)) return r;
+    HIPCHK(c, hipMemcpyAsync(dst, c->bsp_nodes.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
 int rt_download_bvh(rt_ctx* c, rt_gpu_node* nodes, uint32_t cap_nodes, uint32_t* tri_ids, uint32_t cap_ids,
                     uint32_t* nnodes, uint32_t* nids)
 {

@@ -321,6 +321,15 @@ int rt_build_bsp_device(rt_ctx* ctx, uint32_t max_depth, uint32_t max_leaf, rt_b
 int rt_download_bsp(rt_ctx* ctx, uint32_t* tree, float* planes, uint32_t cap_nodes, uint32_t* ids,
                     uint32_t cap_ids, float aabb[8], uint32_t* nnodes, uint32_t* nids);
 
+/* Diagnostics (no reference counterpart; tests/test_gpu_cert_data.py): copy the
+ * BSP walk's 96-B treelets (slot 0 unused, then one per 1-based node M:
+ * content box, nodes M, 2M, 2M+1, 4M..4M+3, and the certified culling's data
+ * -- F bf16 | camera term G f16 << 16, normal-box centre and radius as f16;
+ * rt_bsp_build.hip k_bsp_repack) to dst, (nnodes + 1) * 96 bytes, after
+ * bringing the camera terms up to date for the uniforms' eye (certified
+ * culling).  The size is stored in *bytes (pass dst NULL to query it). */
+int rt_download_bsp_treelets(rt_ctx* ctx, void* dst, uint64_t cap_bytes, uint64_t* bytes);
+
 /* Copy the context's BVH in the reference layout (GpuNode array, bvh_triangles)
  * to host arrays of capacity cap_nodes / cap_ids; the sizes are stored in
  * nnodes / nids (pass NULL arrays to query them). */

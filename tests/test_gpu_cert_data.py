@@ -1,0 +1,157 @@
+"""The data the certified culling's proof rests on (DESIGN.md section 4
+"Certified culling"), as the GPU repack wrote it into the BSP treelets
+(rt_bsp_build.hip k_leaf_boxes / k_node_boxes / k_bsp_repack / k_treelet_hcam),
+checked node by node against an f64 recomputation on the host from the mesh and
+the reference-layout tree (rt_download_bsp):
+
+  * the content box holds every vertex of the subtree's triangles;
+  * F (bf16) <= 1e-10 / E2, E2 the subtree's largest squared edge (inf-norm of
+    the records' f32 edges) -- the shader's |denom| >= 1e-10 floor, normalised;
+  * the normal box [c - r, c + r] (f16) holds n* / E2s for every triangle, n* =
+    e0 x e1 exactly and E2s = E2 rounded up to f32 (the repack's divisor);
+  * the camera term G (f16) <= (H - 128u D1) / Dinf for the uniforms' eye, H the
+    subtree's least |(v0 - eye) . n*| / E_T^2 and D1, Dinf the L1 / L-inf
+    distances of the stored box from the eye.
+
+Rounding the wrong way anywhere in those kernels would break the proof without
+necessarily changing a test frame; this pins each inequality."""
+import numpy as np
+import pytest
+
+from conftest import model
+
+pytestmark = pytest.mark.gpu
+
+U = 2.0 ** -24
+
+
+def _f16(bits):
+    return np.asarray(bits, np.uint16).view(np.float16).astype(np.float64)
+
+
+def _f32_up(x):
+    """smallest f32 >= x (x >= 0, f64)"""
+    f = x.astype(np.float32)
+    lo = f.astype(np.float64) < x
+    f[lo] = np.nextafter(f[lo], np.float32(np.inf))
+    return f.astype(np.float64)
+
+
+def _check(rt, mesh, eye, target):
+    V, N, I, M, L = mesh.arrays()
+    ctx = rt.Context(0)
+    try:
+        ctx.upload_mesh(mesh)
+        ctx.upload_bsp(mesh.bsp_tree())
+        ctx.set_uniforms(rt.make_uniform(tuple(float(x) for x in eye), target, (0.0, 1.0, 0.0), 1.5, 64, 64))
+        tl = ctx.download_bsp_treelets()
+        tree, planes, ids, aabb = ctx.download_bsp()
+    finally:
+        ctx.close()
+    n = tree.shape[0]
+    assert tl.shape == (n + 1, 24)
+
+    # per triangle, from the records' f32 edges (k_tri_records2)
+    P = V[:, :3].astype(np.float32)
+    v0, v1, v2 = P[I[:, 0]], P[I[:, 1]], P[I[:, 2]]
+    e0 = (v1 - v0).astype(np.float64)
+    e1 = (v2 - v0).astype(np.float64)
+    ns = np.cross(e0, e1)   # exact: products of f32 values, differences well inside f64
+    E = np.maximum(np.abs(e0).max(1), np.abs(e1).max(1))
+    E2 = E * E
+    d = v0.astype(np.float64) - eye.astype(np.float64)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        H = np.where(E2 > 0, np.abs((d * ns).sum(1)) / E2, np.inf)
+    vlo = np.minimum(np.minimum(v0, v1), v2).astype(np.float64)
+    vhi = np.maximum(np.maximum(v0, v1), v2).astype(np.float64)
+
+    # subtree aggregates, bottom-up over the heap (node i: children 2i+1, 2i+2),
+    # leaves first (their id ranges tile ids in order)
+    leaf = (tree[:, 0] & 3) == 3
+    cnt = (tree[:, 0] >> 2).astype(np.int64)
+    first = tree[:, 1].astype(np.int64)
+    lv = np.nonzero(leaf & (cnt > 0))[0]
+    order = np.argsort(first[lv], kind="stable")
+    starts = first[lv][order]
+    assert starts[0] == 0 and np.all(np.diff(np.append(starts, len(ids))) == cnt[lv][order])
+
+    def per_leaf(vals, red, fill):
+        out = np.full((n,) + vals.shape[1:], fill)
+        res = np.empty((len(lv),) + vals.shape[1:])
+        res[order] = red.reduceat(vals[ids.astype(np.int64)], starts, axis=0)
+        out[lv] = res
+        return out
+
+    def up(arr, red):
+        dmax = int(np.floor(np.log2(n + 1)))
+        for dd in range(dmax, -1, -1):
+            i = np.arange(2 ** dd - 1, min(2 ** (dd + 1) - 1, n))
+            i = i[(~leaf[i]) & (2 * i + 2 < n)]
+            arr[i] = red(arr[2 * i + 1], arr[2 * i + 2])
+        return arr
+
+    agg_E2 = up(per_leaf(E2, np.maximum, 0.0), np.maximum)
+    agg_H = up(per_leaf(H, np.minimum, np.inf), np.minimum)
+    agg_lo = up(per_leaf(vlo, np.minimum, np.inf), np.minimum)
+    agg_hi = up(per_leaf(vhi, np.maximum, -np.inf), np.maximum)
+    agg_nlo = up(per_leaf(ns, np.minimum, np.inf), np.minimum)
+    agg_nhi = up(per_leaf(ns, np.maximum, -np.inf), np.maximum)
+
+    # reachable nodes (children of interior nodes), 1-based treelet row M = i + 1
+    reach = np.zeros(n, bool)
+    reach[0] = True
+    dmax = int(np.floor(np.log2(n + 1)))
+    for dd in range(dmax + 1):
+        i = np.arange(2 ** dd - 1, min(2 ** (dd + 1) - 1, n))
+        i = i[reach[i] & ~leaf[i] & (2 * i + 2 < n)]
+        reach[2 * i + 1] = reach[2 * i + 2] = True
+    idx = np.nonzero(reach)[0]
+    rows = tl[idx + 1]
+    box = rows[:, :6].view(np.float32).astype(np.float64)
+    F = ((rows[:, 20] & 0xFFFF) << 16).view(np.float32).astype(np.float64)
+    G = _f16((rows[:, 20] >> 16).astype(np.uint16))
+    c = np.stack([_f16(rows[:, 21] & 0xFFFF), _f16(rows[:, 21] >> 16), _f16(rows[:, 22] & 0xFFFF)], 1)
+    r = np.stack([_f16(rows[:, 22] >> 16), _f16(rows[:, 23] & 0xFFFF), _f16(rows[:, 23] >> 16)], 1)
+
+    has = np.isfinite(agg_lo[idx]).all(1)   # subtrees with triangles
+    assert has.sum() > len(idx) // 4
+    # content box
+    assert (box[has, :3] <= agg_lo[idx][has]).all() and (box[has, 3:] >= agg_hi[idx][has]).all()
+    ext = agg_E2[idx] > 0
+    # floor
+    assert (F[ext] <= 1e-10 / agg_E2[idx][ext]).all()
+    assert np.isinf(F[~ext]).all()
+    # normal box
+    E2s = _f32_up(agg_E2[idx][ext])
+    lo_n = agg_nlo[idx][ext] / E2s[:, None]
+    hi_n = agg_nhi[idx][ext] / E2s[:, None]
+    assert (c[ext] - r[ext] <= lo_n).all(), "normal box misses a normal (low side)"
+    assert (c[ext] + r[ext] >= hi_n).all(), "normal box misses a normal (high side)"
+    # camera term
+    dl = np.abs(box[:, :3] - eye.astype(np.float64))
+    dh = np.abs(box[:, 3:] - eye.astype(np.float64))
+    dd = np.maximum(dl, dh)
+    D1, Dinf = dd.sum(1), dd.max(1)
+    fin = np.isfinite(agg_H[idx]) & has
+    with np.errstate(divide="ignore", invalid="ignore"):
+        Gt = np.where(Dinf > 0, (agg_H[idx] - 128 * U * D1) / Dinf, 0.0)
+    Gt = np.maximum(Gt, 0.0)
+    assert (G[fin] <= Gt[fin]).all(), "camera term above its bound"
+    assert (G[fin] >= 0).all()
+    bound = int((G[fin] > 0).sum())
+    print(f"{len(idx)} reachable treelets ({int(has.sum())} with triangles): content boxes, floors, normal boxes "
+          f"and {bound} positive camera terms within their bounds")
+    return bound
+
+
+def test_teapot_treelets(rt):
+    mesh = rt.Mesh.from_obj(model("teapot.obj"))
+    assert _check(rt, mesh, np.array([0.15, 1.5, 6.0], np.float32), (0.0, 1.0, 0.0)) > 0
+
+
+def test_bunny_treelets(rt):
+    assert _check(rt, rt.Mesh.synth_bunny(), np.array([-0.02, 0.11, 0.6], np.float32), (-0.02, 0.1, 0.0)) > 0
+
+
+def test_soup_treelets(rt):
+    assert _check(rt, rt.Mesh.synth_soup(20_000), np.array([0.0, 0.0, 3.0], np.float32), (0.0, 0.0, 0.0)) > 0
