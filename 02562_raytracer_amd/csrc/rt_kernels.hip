@@ -673,6 +673,9 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 #ifndef RT_SHADE_PRIO
 #define RT_SHADE_PRIO 0
 #endif
+#ifndef RT_W7E3_SHADE_PRIO
+#define RT_W7E3_SHADE_PRIO 2
+#endif
 #ifndef RT_AB_NO_CONE
 #define RT_AB_NO_CONE 0
 #endif
@@ -1509,6 +1512,9 @@ k_path(DevScene S, DevLaunch L)
     constexpr bool CLAMP = W8 && !W8E1;
     constexpr bool FAC_AMB = W9 || W8E3;   // ambient = emission * factor
     constexpr uint32_t MAXD = W8E1 ? 10u : 50u;
+    // the shading phase's issue priority (W7E3's short Cornell-box rays shade often:
+    // +0.9 % at 2, profiles/r04/ab_shade_prio.txt; neutral on W9E1's configs)
+    constexpr int SPRIO = MODE == RT_MODE_W7E3 ? RT_W7E3_SHADE_PRIO : RT_SHADE_PRIO;
     // W9E1 draws the next bounce direction after the shadow walk, from the hit
     // the any-hit walk left in the traversal state (resolve() again): the shadow
     // walk draws no random numbers, so the PRNG sequence is the reference's, and
@@ -1639,7 +1645,7 @@ k_path(DevScene S, DevLaunch L)
         {
         // (A/B: RT_SHADE_PRIO raises the wave's issue priority for its shading and refill
         // phase, so lanes are refilled sooner while the other waves trace)
-        if (RT_SHADE_PRIO) __builtin_amdgcn_s_setprio(RT_SHADE_PRIO);
+        if (SPRIO) __builtin_amdgcn_s_setprio(SPRIO);
         // the shading and refill phases read the kernel arguments afresh (kreload)
         const DevScene& Sk = kreload<DevScene>(KARG_S);
         const DevLaunch& Lk = kreload<DevLaunch>(KARG_L);
@@ -1970,7 +1976,7 @@ k_path(DevScene S, DevLaunch L)
             if (lane == 0) cnt.v[C_SHADE_CYC64] += (uint32_t)((now - tstamp) >> 6);
             tstamp = now;
         }
-        if (RT_SHADE_PRIO) __builtin_amdgcn_s_setprio(0);
+        if (SPRIO) __builtin_amdgcn_s_setprio(0);
         if (__ballot(st != ST_IDLE) == 0) break;
     }
     flush_counters(cnt, L.counters, COUNT);
@@ -2704,10 +2710,10 @@ size_t bvh_deep_bytes(int num_cus, int waves_per_cu)
 template <int MODE, int TRAV, bool COUNT>
 static void launch_path(const DevScene& s, const DevLaunch& l, int grid, size_t lds, hipStream_t st)
 {
-    // W9E1's BSP walk (configs 3-5) has a fast-margin instantiation: a context whose
+    // W9E1's and W7E3's BSP walks (configs 2-5) have a fast-margin instantiation: a context whose
     // culling is not certified (cull_k1 = 0: fast, or off with its +inf gap) skips the
     // certified terms (round 3's trip).  The other modes run the generic formula.
-    if constexpr (MODE == RT_MODE_W9E1 && TRAV == RT_TRAVERSE_BSP) {
+    if constexpr ((MODE == RT_MODE_W9E1 || MODE == RT_MODE_W7E3) && TRAV == RT_TRAVERSE_BSP) {
         if (s.cull_k1 == 0.0f) {
             hipLaunchKernelGGL((k_path<MODE, TRAV, COUNT, false>), dim3(grid), dim3(256), lds, st, s, l);
             return;

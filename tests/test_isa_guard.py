@@ -22,7 +22,8 @@ BUDGET = {
     "k_pathILi4ELi0ELb0ELb1": 0,
     "k_pathILi4ELi0ELb0ELb0": 0,   # W9E1, BSP, the fast-margin instantiation
     "k_pathILi4ELi1ELb0ELb1": 0,   # W9E1, BVH at 8 waves/SIMD (4 before the round-2 spill cuts)
-    "k_pathILi3ELi0ELb0ELb1": 0,   # W7E3, BSP at 7 waves/SIMD
+    "k_pathILi3ELi0ELb0ELb1": 0,
+    "k_pathILi3ELi0ELb0ELb0": 0,   # W7E3, BSP, the fast-margin instantiation   # W7E3, BSP at 7 waves/SIMD
 }
 
 
@@ -57,7 +58,8 @@ WHOLE_BUDGET = {
     "k_pathILi4ELi0ELb0ELb1": (108, 93),    # W9E1, BSP
     "k_pathILi4ELi0ELb0ELb0": (88, 99),     # W9E1, BSP, the fast-margin instantiation
     "k_pathILi4ELi1ELb0ELb1": (80, 77),     # W9E1, BVH
-    "k_pathILi3ELi0ELb0ELb1": (64, 56),     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
+    "k_pathILi3ELi0ELb0ELb1": (64, 56),
+    "k_pathILi3ELi0ELb0ELb0": (68, 63),     # W7E3, BSP, the fast-margin instantiation     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
 }
 
 
