@@ -14,6 +14,7 @@ for step in "$@"; do
       timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1
       rc=$?; tail -3 $OUT/pytest_gpu.log; grep -E "FAILED|ERROR" $OUT/pytest_gpu.log | head -20
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi ;;
+    c2) bash tools/measure.sh $TAG/c2 --config 2 --no-cpu-baseline || exit 1 ;;
     c3) bash tools/measure.sh $TAG/c3 || exit 1 ;;
     c3fast) bash tools/measure.sh $TAG/c3fast --bsp-cull 2 || exit 1 ;;
     c4) bash tools/measure.sh $TAG/c4 --config 4 --no-cpu-baseline || exit 1 ;;
