@@ -141,6 +141,7 @@ SIGNATURES = {
     "rt_timer_stop": (C.c_int, [vp, f32p]),
     "rt_frame_rgba8": (C.c_int, [vp, vp, C.c_uint32, vp]),
     "rt_kernel_time": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), u32p]),
+    "rt_gather_time": (C.c_int, [vp, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), u32p]),
     "rt_build_bvh_device": (C.c_int, [vp, C.c_uint32, C.POINTER(BvhBuildTimes)]),
     "rt_build_bsp_device": (C.c_int, [vp, C.c_uint32, C.c_uint32, C.POINTER(BspBuildTimes)]),
     "rt_download_bsp": (C.c_int, [vp, u32p, f32p, C.c_uint32, u32p, C.c_uint32, f32p, u32p, u32p]),
@@ -203,6 +204,8 @@ def lib():
             raise RuntimeError(f"{LIB_PATH} is missing: run __graft_entry__.build() (make -C 02562_raytracer_amd)")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("RT_LIBRARY") and not hasattr(L, name):
+                continue   # an A/B variant built from an earlier tree (tools/ab.sh) may lack a newer entry point
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args

@@ -468,6 +468,16 @@ class Context:
         self._chk(F.lib().rt_kernel_time(self._h, int(reset), C.byref(ms), C.byref(n)))
         return ms.value, n.value
 
+    def gather_time(self, reset=True):
+        """(transfer ms, unpack ms, calls) of the frame assembly timed since the last
+        reset (rt_gather_time: rt_gather_tiles' RCCL transfers and every unpack;
+        RT_OPT_KERNEL_TIMING must be on); synchronizes."""
+        tx = C.c_double()
+        up = C.c_double()
+        n = C.c_uint32()
+        self._chk(F.lib().rt_gather_time(self._h, int(reset), C.byref(tx), C.byref(up), C.byref(n)))
+        return tx.value, up.value, n.value
+
     def selftest_math(self, n=1 << 20, lo=-4.0, hi=4.0):
         bad = C.c_uint32()
         self._chk(F.lib().rt_selftest_math(self._h, n, lo, hi, C.byref(bad)))

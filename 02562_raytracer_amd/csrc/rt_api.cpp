@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <string>
 #include <thread>
@@ -115,6 +116,11 @@ struct rt_ctx {
     bool ktiming = false;
     std::vector<hipEvent_t> kev;
     size_t kused = 0;   // events recorded since the last reset (2 per launch)
+    // ... and around the tile gather's transfers and the unpack kernel (rt_gather_time):
+    // triples {before the transfers, after them, after the unpack} per call (an
+    // rt_unpack_tiles call: its transfer part is empty)
+    std::vector<hipEvent_t> gev;
+    size_t gused = 0;
     // rt_comm_init: the tile gather's RCCL communicator (rt_gather_tiles)
     // RT_OPT_ASYNC_FOLD: the fold and its consumers on a second stream, the
     // per-sample scratch double-buffered (ev_free[b]: the fold that last read buffer b)
@@ -285,6 +291,7 @@ void rt_destroy(rt_ctx* c)
         if (e) (void)hipEventDestroy(e);
     if (c->fold_stream) (void)hipStreamDestroy(c->fold_stream);
     for (hipEvent_t e : c->kev) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->gev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->own) (void)hipStreamDestroy(c->own);
@@ -552,9 +559,9 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
     // with 32-bit offsets (DESIGN.md "Data layout in HBM"), laid out on the
     // device by launch_bsp_repack from the reference arrays (the same code as
     // rt_build_bsp_device):
-    //  * treelet of node M (1-based heap index), 80 B at 80*M: M's content box
-    //    and the 8-B nodes {M | 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3} -- everything
-    //    a 3-level walk from M reads;
+    //  * treelet of node M (1-based heap index), 96 B at 96*M: M's content box,
+    //    the 8-B nodes {M | 2M, 2M+1 | 4M, 4M+1 | 4M+2, 4M+3} and the certified
+    //    culling's 16 B of subtree data -- everything a 3-level walk from M reads;
     //  * 8-B node: interior {axis, plane bits}; leaf {3 | (48*count) << 2, byte
     //    offset of its first record} (children implicit: 2i+1, 2i+2 0-based);
     //  * record k (treeIds slot k): 48 B {v0, e0, e1, n} at rec_off + 48*k.
@@ -562,7 +569,8 @@ int rt_upload_bsp(rt_ctx* c, const float aabb[8], const uint32_t* tree, const fl
     const size_t rec_off = (slots * rtk::BSP_TREELET_BYTES + 255) & ~(size_t)255;
     const size_t total = rec_off + (size_t)nids * 48;
     if (total >= ((size_t)1 << 32))
-        return fail(c, RT_E_UNSUPPORTED, "rt_upload_bsp: BSP treelets + records must stay below 4 GiB (max_depth <= 24)");
+        return fail(c, RT_E_UNSUPPORTED, "rt_upload_bsp: BSP treelets + records must stay below 4 GiB (96-B treelets: "
+                                              "max_depth 24 takes 3.2 GB, leaving room for ~22M records)");
     if ((r = upload(c, c->bsp_ref_tree, tree, (size_t)nnodes * 16))) return r;
     if ((r = upload(c, c->bsp_ref_planes, planes, (size_t)nnodes * 4))) return r;
     if ((r = upload(c, c->bsp_ids, ids, (size_t)nids * 4))) return r;
@@ -759,8 +767,8 @@ int rt_download_bsp_treelets(rt_ctx* c, void* dst, uint64_t cap_bytes, uint64_t*
     if (bytes) *bytes = n;
     if (!dst) return RT_OK;
     if (cap_bytes < n) return fail(c, RT_E_INVALID, "rt_download_bsp_treelets: buffer too small");
+    if (int r = set_dev(c)) return r;   // (first: ensure_hcam may launch the camera-term kernels)
     if (int r = ensure_hcam(c)) return r;
-    if (int r = set_dev(c)) return r;
     HIPCHK(c, hipMemcpyAsync(dst, c->bsp_nodes.p, n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return RT_OK;
@@ -816,6 +824,27 @@ int rt_set_environment(rt_ctx* c, const float rgb[3])
     if (!c || !rgb) return RT_E_INVALID;
     memcpy(c->env, rgb, sizeof c->env);
     return RT_OK;
+}
+
+// The gather/unpack event triples (RT_OPT_KERNEL_TIMING, rt_gather_time): the
+// next pooled event of the current call, recorded on stream s (nullptr: off).
+// The first event of a triple reserves all three (a call records the other two
+// only when the first was recorded, so the pool stays in whole triples).
+static hipEvent_t gather_event(rt_ctx* c, hipStream_t s)
+{
+    if (!c->ktiming) return nullptr;
+    if (c->gused % 3 == 0) {
+        if (c->gused >= 3 * 4096) return nullptr;
+        while (c->gev.size() < c->gused + 3) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return nullptr;
+            c->gev.push_back(e);
+        }
+    }
+    hipEvent_t e = c->gev[c->gused];
+    (void)hipEventRecord(e, s);
+    c->gused++;
+    return e;
 }
 
 // Launch the traversal kernel, bracketed by a pair of pooled events when
@@ -904,7 +933,10 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bvh_nnodes = c->bvh_nnodes;
     // the culling margin as data (rt_internal.h DevScene, rt_kernels.hip bsp_box_miss)
     S.bsp_cull_gap = c->bsp_cull != RT_BSP_CULL_OFF ? 0x1p-18f : INFINITY;
-    if (c->bsp_cull == RT_BSP_CULL_FAST) {
+    S.bsp_cull_emax = c->bsp_cull != RT_BSP_CULL_OFF ? FLT_MAX : INFINITY;
+    // off: the fast formula's constants (k1 = 0 picks k_path's fast-margin
+    // instantiation, launch_path); the +inf gap culls nothing either way
+    if (c->bsp_cull != RT_BSP_CULL_CERTIFIED) {
         S.cull_k1 = 0.0f;
         S.cull_k3 = 0.0f;
         S.cull_ko = 0x1p-10f;
@@ -964,7 +996,10 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
             return fail(c, RT_E_NOT_READY, "rt_render: W6E1/PROJECT need the BSP root AABB");
     }
     if (!L.accum) return fail(c, RT_E_INVALID, "rt_render: accum buffer required");
-    if (int r = set_dev_nojoin(c)) return r;
+    // a path mode orders itself against a pending fold (double-buffered samples,
+    // the fold stream); every other mode writes accum / ids on the context stream
+    // itself, so a fold of an earlier path render still pending there is joined first
+    if (int r = path ? set_dev_nojoin(c) : set_dev(c)) return r;
     if (int r = ensure_hcam(c)) return r;
     const rtk::DevScene S = dev_scene(c);
     L.u = c->u;
@@ -1164,9 +1199,12 @@ int rt_unpack_tiles(rt_ctx* c, uint32_t width, uint32_t height, uint32_t nranks,
     hipStream_t os;
     if (int r = out_stream(c, &os)) return r;
     const uint32_t lt = rt_tileset_local_tiles(width, height, nranks);
+    const bool tm = gather_event(c, os) != nullptr;   // (no transfers: the first two events coincide)
+    if (tm) gather_event(c, os);
     int r = rtk::launch_unpack(width, height, nranks, lt, reinterpret_cast<const float4*>(packed_accum), packed_ids,
                                reinterpret_cast<float4*>(frame_accum), frame_ids, os);
     if (r) return fail(c, r, "rt_unpack_tiles: launch failed");
+    if (tm) gather_event(c, os);
     return RT_OK;
 }
 
@@ -1280,6 +1318,7 @@ int rt_gather_tiles(rt_ctx* c, uint32_t width, uint32_t height, const float* loc
     if (int r = out_stream(c, &os)) return r;
     const Rccl& R = rccl();
     const size_t px = (size_t)rt_tileset_local_tiles(width, height, N) * 64u;
+    const bool tm = gather_event(c, os) != nullptr;   // transfers start (RT_OPT_KERNEL_TIMING)
     if (!root) {
         // one group: this rank's accumulation and ids to rank 0
         ncclResult_t e = R.group_start();
@@ -1287,6 +1326,10 @@ int rt_gather_tiles(rt_ctx* c, uint32_t width, uint32_t height, const float* loc
         if (!e && local_ids) e = R.send(local_ids, px, ncclUint32, 0, c->comm, os);
         const ncclResult_t e2 = R.group_end();
         if (e || e2) return fail(c, RT_E_DEVICE, "rt_gather_tiles send: " + nccl_msg(R, e ? e : e2));
+        if (tm) {   // sent; no unpack on this rank
+            gather_event(c, os);
+            gather_event(c, os);
+        }
         return RT_OK;
     }
     // rank 0: every peer's packed tiles, rank-major beside its own (slot 0), in one group
@@ -1305,10 +1348,32 @@ int rt_gather_tiles(rt_ctx* c, uint32_t width, uint32_t height, const float* loc
         const ncclResult_t e2 = R.group_end();
         if (e || e2) return fail(c, RT_E_DEVICE, "rt_gather_tiles recv: " + nccl_msg(R, e ? e : e2));
     }
+    if (tm) gather_event(c, os);   // received
     int r = rtk::launch_unpack(width, height, N, (uint32_t)(px / 64), reinterpret_cast<const float4*>(ga),
                                local_ids ? gi : nullptr, reinterpret_cast<float4*>(frame_accum),
                                local_ids ? frame_ids : nullptr, os);
     if (r) return fail(c, r, "rt_gather_tiles: unpack launch failed");
+    if (tm) gather_event(c, os);   // unpacked
+    return RT_OK;
+}
+
+int rt_gather_time(rt_ctx* c, int reset, double* transfer_ms, double* unpack_ms, uint32_t* calls)
+{
+    if (!c) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    double tx = 0.0, up = 0.0;
+    for (size_t i = 0; i + 2 < c->gused; i += 3) {
+        HIPCHK(c, hipEventSynchronize(c->gev[i + 2]));
+        float a = 0.0f, b = 0.0f;
+        HIPCHK(c, hipEventElapsedTime(&a, c->gev[i], c->gev[i + 1]));
+        HIPCHK(c, hipEventElapsedTime(&b, c->gev[i + 1], c->gev[i + 2]));
+        tx += a;
+        up += b;
+    }
+    if (transfer_ms) *transfer_ms = tx;
+    if (unpack_ms) *unpack_ms = up;
+    if (calls) *calls = (uint32_t)(c->gused / 3);
+    if (reset) c->gused = 0;
     return RT_OK;
 }
 

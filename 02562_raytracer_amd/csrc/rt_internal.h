@@ -52,6 +52,11 @@ struct DevScene {
     // the eye the treelets' camera terms are for (rt_bsp_build.hip
     // launch_bsp_camera): rays starting exactly there use them (NaN: none)
     float cam_eye[3];
+    // the cap of the cull's gap tolerance (bsp_box_miss): FLT_MAX with culling on, so a
+    // slab that is +-inf (an axis whose direction component is exactly zero and whose
+    // origin coordinate lies outside the grown box) culls; +inf with culling off
+    // (kept last: a field added mid-struct once moved the trip loop into spills)
+    float bsp_cull_emax;
 };
 
 // Work mapping + outputs of one launch.

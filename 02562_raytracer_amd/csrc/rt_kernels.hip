@@ -651,9 +651,17 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // accept one of the subtree's triangles -- its f32 rounding, including
 // |denom| >= 1e-10 at grazing angles -- so the cull is exact for every ray.
 // Fast mode (k1 = k3 = 0, ko and dscene 2^-10): the round-3 margin, not a bound.
-// An axis whose direction component is below the shader's 1e-8 cut (inv is
-// then +-1e8 or the NaN flag, see bsp_inv1) constrains nothing: the NaN drops
-// out of fminf / fmaxf.
+// Axes whose direction component is below the shader's 1e-8 cut (bsp_inv1):
+//  * exactly zero (+-0; inv is +1e8 = RN(1/1e-8)): every point o + dist*w of the
+//    ray has that coordinate o_a exactly, so the slab is a yes/no test of o_a
+//    against the grown box -- inv * inf makes its products +-inf (o_a outside:
+//    both ends of the slab at +inf or at -inf, the interval is empty; inside:
+//    -inf..+inf, no constraint; a zero product is NaN and constrains nothing).
+//    An infinite end culls against the gap tolerance's cap S.bsp_cull_emax
+//    (FLT_MAX; +inf with culling off).  W9E1's shadow rays (0, 1, 0)
+//    (w9e1.wgsl:442-446) are the common case;
+//  * nonzero, |w_a| <= 1e-8 (inv is the NaN flag): constrains nothing, the NaN
+//    drops out of fminf / fmaxf.
 // RT_BSP_CULL 0 compiles the test out (A/B builds; RT_OPT_BSP_CULL then has no effect).
 #ifndef RT_BSP_CULL
 #define RT_BSP_CULL 1
@@ -745,7 +753,7 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
     const v2f mm = {-m, m};
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : __builtin_nanf("");
+        const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : iv[a] * __builtin_inff();
         const v2f dd = {dl[a], dh[a]};
         const v2f t = (dd + mm) * ib;
         tn = __builtin_fmaxf(tn, __builtin_fminf(t.x, t.y));
@@ -754,14 +762,16 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
 #else
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : __builtin_nanf("");
+        const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : iv[a] * __builtin_inff();   // +1e8: a zero component
         const float t1 = (dl[a] - m) * ib, t2 = (dh[a] + m) * ib;
         tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
         tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
     }
 #endif
     // a clear gap: the rounding of the slab products cannot close it
-    const float e = (rt_absf(tn) + rt_absf(tf)) * S.bsp_cull_gap;
+    // (capped: an infinite slab end from a zero direction component must still
+    // show a gap; a finite product cannot reach the cap)
+    const float e = __builtin_fminf((rt_absf(tn) + rt_absf(tf)) * S.bsp_cull_gap, S.bsp_cull_emax);
     // the interval the subtree's content can be hit in, widened by the same
     // tolerance (RT_BSP_CLIP; culling off: e = inf or NaN, lo = tmin, hi = tmax)
     lo = __builtin_fmaxf(tmin, tn - e);
@@ -885,11 +895,18 @@ __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3
 // of magnitude < 1e-8 (denom is +1e-8 there) or NaN; those components get a
 // negative NaN, which sends every decision on that axis to the exact path
 // (NaN compares false) with the right near child.
+// +1e8 marks an exactly zero component for the subtree cull (bsp_box_miss): every
+// other component of magnitude <= 1e-8 (whose reciprocal would also be +-1e8)
+// gets the NaN flag with its near child in the sign bit; the exact path divides
+// by the same denominator, so its decisions do not change.
 __device__ __forceinline__ float bsp_inv1(float ad)
 {
     const float r = 1.0f / (rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad);   // RN(1/denom): rt_div_by_recip's reciprocal
     const bool near_right = !(ad >= 0.0f);
-    return (near_right && !(__float_as_uint(r) >> 31)) ? __uint_as_float(0xFFC00000u) : r;
+    const bool tiny = (rt_absf(ad) <= 1.0e-8f) & (ad != 0.0f);
+    return ((near_right && !(__float_as_uint(r) >> 31)) || tiny)
+               ? __uint_as_float(near_right ? 0xFFC00000u : 0x7FC00000u)
+               : r;
 }
 __device__ __forceinline__ f3 bsp_inv(const f3 d) { return V(bsp_inv1(d.x), bsp_inv1(d.y), bsp_inv1(d.z)); }
 

@@ -7,11 +7,16 @@
 //   rt_render --scene NAME [--res WxH] [--spp N | --samples N] [--keys K1,K2 --updates N]
 //             [--selection K] [--subdiv K] [--camera-constant C] [--device-build]
 //             [--env-rgba FILE --env-size WxH] [--models DIR] [--out PREFIX]
-//   rt_render ... --nranks N --rank R --comm-file PATH [--device D]
+//   rt_render ... --nranks N --rank R --comm-file PATH [--comm-token T] [--device D]
 //                                        (one process per GPU: rank R renders its
 //                                        interleaved tiles, rank 0 gathers the frame
 //                                        over RCCL and writes it; rank 0 publishes the
-//                                        communicator id in PATH; device defaults to R)
+//                                        communicator id in PATH, tagged with T -- any
+//                                        string unique to the launch, e.g. a job id, the
+//                                        same on every rank; default $RT_COMM_TOKEN --
+//                                        and the other ranks take only a file with
+//                                        their T, never a previous launch's; without a
+//                                        token PATH must be fresh; device defaults to R)
 //   rt_render --camera-test K1,K2 N      (CPU: eye after N controller updates)
 //   rt_render --jitter SUBDIV HEIGHT     (CPU: the jitter table)
 //
@@ -22,6 +27,7 @@
 #include <chrono>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -94,22 +100,35 @@ static void write_file(const std::string& path, const void* p, size_t n)
     if (!f) throw Error(RT_E_INVALID, "cannot write " + path);
 }
 
-// the communicator id through a file: rank 0 writes it (then renames, so a
-// reader never sees a partial file), the other ranks wait for it
-static void publish_comm_id(const std::string& path, uint8_t id[RT_COMM_ID_BYTES], uint32_t rank)
+// the communicator id through a file: rank 0 writes "RTCOMMID <token>\n" and the
+// id (to PATH.tmp, then renames, so a reader never sees a partial file), the
+// other ranks wait for a file that carries their own token.  A file left by an
+// earlier launch (another token) is never taken: its id has no rank 0 any more,
+// and ncclCommInitRank would wait for it forever.
+static void publish_comm_id(const std::string& path, const std::string& token, uint8_t id[RT_COMM_ID_BYTES],
+                            uint32_t rank)
 {
+    if (token.find('\n') != std::string::npos) throw Error(RT_E_INVALID, "--comm-token: no newlines");
+    const std::string head = "RTCOMMID " + token + "\n";
     if (rank == 0) {
+        std::remove(path.c_str());   // a stale file goes before the new id exists
         if (int r = rt_comm_unique_id(id)) throw Error(r, rt_last_error(nullptr));
-        write_file(path + ".tmp", id, RT_COMM_ID_BYTES);
+        std::string buf = head;
+        buf.append(reinterpret_cast<const char*>(id), RT_COMM_ID_BYTES);
+        write_file(path + ".tmp", buf.data(), buf.size());
         if (std::rename((path + ".tmp").c_str(), path.c_str()) != 0) throw Error(RT_E_INVALID, "cannot publish " + path);
         return;
     }
     for (int i = 0; i < 1200; i++) {   // up to 2 minutes
         std::ifstream f(path, std::ios::binary);
-        if (f && f.read(reinterpret_cast<char*>(id), RT_COMM_ID_BYTES)) return;
+        std::string buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+        if (buf.size() == head.size() + RT_COMM_ID_BYTES && buf.compare(0, head.size(), head) == 0) {
+            std::memcpy(id, buf.data() + head.size(), RT_COMM_ID_BYTES);
+            return;
+        }
         std::this_thread::sleep_for(std::chrono::milliseconds(100));
     }
-    throw Error(RT_E_NOT_READY, "no communicator id in " + path);
+    throw Error(RT_E_NOT_READY, "no communicator id for token '" + token + "' in " + path);
 }
 
 static std::string default_models_dir(const char* argv0)
@@ -185,7 +204,9 @@ int main(int argc, char** argv)
         RenderState rs(gpu, find_scene(*name), opt);
         if (const std::string* cf = arg("--comm-file")) {
             uint8_t id[RT_COMM_ID_BYTES];
-            publish_comm_id(*cf, id, rank);
+            const char* et = std::getenv("RT_COMM_TOKEN");
+            const std::string token = arg("--comm-token") ? *arg("--comm-token") : (et ? et : "");
+            publish_comm_id(*cf, token, id, rank);
             rs.set_tiling(nranks, rank, id);
         }
         std::vector<uint8_t> env;

@@ -186,6 +186,15 @@ def all_reduce(dist, t, op):
     return h.to(t.device)
 
 
+def all_gather(dist, t, world):
+    """world x len(t) array of every rank's t (RCCL on the device, gloo through host memory)."""
+    import torch
+    src = t if dist.get_backend() == "nccl" else t.cpu()
+    out = [torch.empty_like(src) for _ in range(world)]
+    dist.all_gather(out, src)
+    return torch.stack(out).cpu().numpy()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -307,6 +316,8 @@ def main():
     frame = torch.empty((H, W, 4), dtype=torch.float32, device=dev)
     frame_ids = torch.empty((H, W), dtype=torch.int32, device=dev)
 
+    host_gather_s = [0.0]   # gloo rehearsal: the host-blocking torch gather, wall time per timed step
+
     def step(events=None):
         if events is not None:
             events[0].record(stream)
@@ -317,7 +328,11 @@ def main():
             ctx.gather_tiles(W, H, acc_local.data_ptr(), ids_local.data_ptr(),
                              frame.data_ptr() if rank == 0 else None, frame_ids.data_ptr() if rank == 0 else None)
         elif use_dist:
-            tiling.gather_tiles(dist, acc_local, ids_local, acc_all, ids_all)
+            stream.synchronize()   # (the gather's .cpu() would wait for the render anyway)
+            tg = time.perf_counter()
+            tiling.gather_tiles(dist, acc_local, ids_local, acc_all, ids_all)   # (blocks the host: .cpu())
+            if events is not None:
+                host_gather_s[0] += time.perf_counter() - tg
             if rank == 0:
                 ctx.unpack_tiles(W, H, world, acc_all.data_ptr(), ids_all.data_ptr(), frame.data_ptr(),
                                  frame_ids.data_ptr())
@@ -358,6 +373,9 @@ def main():
     # step's other kernels -- fold, unpack -- and the gather are excluded)
     ctx.set_option(rt._ffi.RT_OPT_KERNEL_TIMING, 1)
     ctx.kernel_time(reset=True)
+    gather_timing = hasattr(rt._ffi.lib(), "rt_gather_time")   # (an A/B variant of an earlier tree has none)
+    if gather_timing:
+        ctx.gather_time(reset=True)
     if use_dist:
         dist.barrier()
     torch.cuda.synchronize(dev)
@@ -372,6 +390,11 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kern_total, launches = ctx.kernel_time(reset=True)
+    # the frame's assembly, per rank: rt_gather_tiles' RCCL transfers (HIP events;
+    # under gloo the host-timed torch gather) and the unpack kernel (rank 0)
+    xfer_total, unpack_total, _ = ctx.gather_time(reset=True) if gather_timing else (0.0, 0.0, 0)
+    if use_dist and not native_gather:
+        xfer_total = host_gather_s[0] * 1e3
     ctx.set_option(rt._ffi.RT_OPT_KERNEL_TIMING, 0)
     launches_per_step = launches // args.steps
     kern_ms = kern_total / max(1, launches)   # average k_path launch
@@ -381,6 +404,13 @@ def main():
     if use_dist:
         t = all_reduce(dist, t, dist.ReduceOp.MAX)
     elapsed, kern_ms, render_ms = [float(x) for x in t.cpu().numpy()]
+    # per-rank step breakdown (ms per step): k_path, the gather's transfers, the unpack
+    mine = torch.tensor([kern_total / args.steps, xfer_total / args.steps, unpack_total / args.steps],
+                        dtype=torch.float64, device=dev)
+    if use_dist:
+        per_rank = all_gather(dist, mine, world)
+    else:
+        per_rank = mine.cpu().numpy()[None, :]
 
     value = rays[0] * args.steps / elapsed / 1e6
     if rank == 0:
@@ -389,6 +419,7 @@ def main():
         # rank 0's share (profiles/pmc_summary.json key _n<N>, measured with --rank-share N)
         bytes_per_launch = rays[4] / (world if use_dist else 1) / max(1, launches_per_step)
         cull = args.bsp_cull if args.bsp_cull is not None else rt._ffi.RT_BSP_CULL_CERTIFIED
+        cull_name = {0: "off", 1: "certified", 2: "fast"}[cull] if trav == "BSP" else None
         roof = roofline(pmc_key(W, H, spp, trav, nsplit, args.config, cull), kern_ms_own, bytes_per_launch, args.config,
                         f"k_path<{wl.mode},{trav}>")
         roof["launches_per_step"] = launches_per_step
@@ -405,6 +436,8 @@ def main():
                                    f"{trav}{' D20/leaf4' if trav == 'BSP' else ' leaf4'}, {W}x{H}, {spp} spp/step",
                        "resolution": [W, H], "spp": spp, "traversal": trav, "ntris": mesh.ntris, "mode": wl.mode,
                        "parallelism": f"tiles8x8/{nsplit}",
+                       # RT_OPT_BSP_CULL: the subtree culling (a different k_path instantiation per mode)
+                       "bsp_cull": cull_name,
                        "world_size": dist.get_world_size() if use_dist else 1,
                        "backend": dist.get_backend() if use_dist else None,
                        "fold": "async (RT_OPT_ASYNC_FOLD)" if args.async_fold else "sync",
@@ -414,6 +447,17 @@ def main():
                           if share > 1 else {})},
             "roofline": roof,
             "cpu_baseline": cpu,
+            # where each rank's step goes (ms per step, HIP events on the stream the work
+            # runs on; the gloo rehearsal's gather is host wall time): its k_path
+            # launches, the tile gather's transfers, the unpack (rank 0); the rest of
+            # ms_per_step is k_fold, the barrier and launch gaps
+            "step_breakdown": {
+                "k_path_ms": [round(float(x), 3) for x in per_rank[:, 0]],
+                "gather_ms": [round(float(x), 3) for x in per_rank[:, 1]],
+                "unpack_ms": [round(float(x), 3) for x in per_rank[:, 2]],
+                "gather_timer": ("rt_gather_time (HIP events around the RCCL transfers)" if native_gather else
+                                 "host wall time of torch.distributed.gather (gloo)" if use_dist else None),
+            },
             "rays_per_step": {"primary": int(rays[1]), "shadow": int(rays[2]), "bounce": int(rays[3])},
             # this rank's counting step: every launch of one step summed (config 5
             # at 1024 spp is 8 launches of 128 spp, roofline.launches_per_step)

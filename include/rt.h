@@ -176,7 +176,8 @@ typedef struct rt_ray_counts {
 #define RT_OPT_ASYNC_FOLD     10  /* 0 (default) / 1: pipelined frames.  The path tracers' progressive fold (the
                                      last step of rt_render / rt_render_tiles) runs on a second, context-owned
                                      stream, and so do the calls that consume its outputs (rt_unpack_tiles,
-                                     rt_gather_tiles, rt_frame_rgba8); the per-sample scratch is double-buffered.
+                                     rt_gather_tiles; rt_frame_rgba8 joins that stream and runs on the
+                                     context stream); the per-sample scratch is double-buffered.
                                      The next render's traversal kernel then overlaps this frame's fold and
                                      gather.  rt_synchronize, the memcpy/memset calls and every other entry point
                                      wait for that stream first; a caller reading the outputs through its own
@@ -243,6 +244,15 @@ int rt_timer_stop(rt_ctx* ctx, float* ms);   /* synchronizes */
  * duration and the number of launches since the last reset (reset != 0
  * clears them).  At most 4096 launches are kept between resets. */
 int rt_kernel_time(rt_ctx* ctx, int reset, double* total_ms, uint32_t* launches);
+
+/* The same for the frame's assembly (RT_OPT_KERNEL_TIMING): HIP events on the
+ * output stream around the RCCL transfers of rt_gather_tiles (rank 0: the copy of
+ * its own tiles and every peer's receive; another rank: its send) and around the
+ * unpack kernel (rt_gather_tiles on rank 0, rt_unpack_tiles).  Synchronizes and
+ * returns the summed times and the number of calls since the last reset (at
+ * most 4096 calls are kept between resets).  For a multi-GPU host's per-rank
+ * diagnostics (bench.py's N>1 line). */
+int rt_gather_time(rt_ctx* ctx, int reset, double* transfer_ms, double* unpack_ms, uint32_t* calls);
 
 /* ---- uploads (replace the src/bindings/ create_buffer_init calls) ------------- */
 

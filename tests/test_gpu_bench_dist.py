@@ -46,9 +46,29 @@ def _bench(nproc, out, launcher=None, backend="gloo"):
     return json.loads(lines[0]), np.load(out)
 
 
+def _check_breakdown(line, world):
+    # the per-rank step breakdown the N>1 line carries: every rank's
+    # k_path time, its part of the gather, the unpack on rank 0; none exceeds the step
+    b = line["step_breakdown"]
+    assert len(b["k_path_ms"]) == len(b["gather_ms"]) == len(b["unpack_ms"]) == world
+    for r in range(world):
+        assert b["k_path_ms"][r] > 0
+        assert b["k_path_ms"][r] + b["gather_ms"][r] + b["unpack_ms"][r] <= line["ms_per_step"] * 1.05 + 0.5, b
+        if r > 0:
+            assert b["gather_ms"][r] > 0 and b["unpack_ms"][r] == 0, b
+    assert b["unpack_ms"][0] > 0
+    # rank 0's k_path launches are the line's roofline kernel time x launches per step
+    roof = line["roofline"]
+    assert abs(b["k_path_ms"][0] - roof["kernel_ms"] * roof["launches_per_step"]) <= 0.01 + 1e-3 * b["k_path_ms"][0]
+
+
 def test_two_rank_bench_frame_equals_one_rank(tmp_path, rt, oracle):
     one, f1 = _bench(1, str(tmp_path / "n1.npz"))
     two, f2 = _bench(2, str(tmp_path / "n2.npz"))
+    _check_breakdown(one, 1)
+    _check_breakdown(two, 2)
+    assert two["step_breakdown"]["gather_timer"].startswith("host wall time")
+    assert one["config"]["bsp_cull"] == "certified"
     assert two["n_gpus"] == 2 and two["config"]["world_size"] == 2 and two["config"]["backend"] == "gloo"
     assert one["config"]["world_size"] == 1
     # every ray counted once across the ranks
@@ -70,6 +90,7 @@ def test_eight_rank_bench_frame_equals_one_rank(tmp_path):
     one, f1 = _bench(1, str(tmp_path / "n1.npz"))
     eight, f8 = _bench(8, str(tmp_path / "n8.npz"))
     assert eight["n_gpus"] == 8 and eight["config"]["world_size"] == 8
+    _check_breakdown(eight, 8)
     assert eight["rays_per_step"] == one["rays_per_step"]
     assert np.array_equal(f1["ids"], f8["ids"])
     assert np.array_equal(f1["accum"].view(np.uint32), f8["accum"].view(np.uint32))
@@ -85,6 +106,9 @@ def test_one_rank_rccl_bench_frame_equals_plain_run(tmp_path):
     one, f1 = _bench(1, str(tmp_path / "n1.npz"))
     nc, fn = _bench(1, str(tmp_path / "nccl1.npz"), launcher=True, backend="nccl")
     assert nc["config"]["backend"] == "nccl" and nc["config"]["world_size"] == 1
+    _check_breakdown(nc, 1)
+    assert nc["step_breakdown"]["gather_timer"].startswith("rt_gather_time")
+    assert nc["step_breakdown"]["gather_ms"][0] > 0   # rank 0's copy of its own tiles
     assert nc["config"]["gather"].startswith("rt_gather_tiles")
     assert one["config"]["backend"] is None
     assert nc["rays_per_step"] == one["rays_per_step"]

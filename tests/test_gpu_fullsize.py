@@ -8,7 +8,11 @@ not depend on size, plus the oracle where it finishes in seconds:
     hands out units in a different order each run; the fold does not care);
   - the 8-rank tile split of the frame, gathered and unpacked, equals the
     single-device frame (the N>1 data path of bench.py, all ranks on one GPU);
-  - 24 pixels spread over the frame equal the oracle at all 256 iterations.
+  - 24 pixels spread over the frame equal the oracle at all 256 iterations;
+  - the whole frame at its BASELINE 256 spp, rendered with the default
+    (certified) culling exactly as the bench renders it, equals the oracle's 256
+    iterations in every pixel's accumulation bits and primary id (the oracle
+    walks every node, as bsp.wgsl does: ~26 s on the box's 16 threads).
 * config 5 (10M-triangle soup, 3840x2160, W9E1, BSP): split identity at 2 spp.
 """
 import numpy as np
@@ -52,6 +56,19 @@ def test_config3_256spp_split_and_rerun_identity(bunny):
         o = bunny.render_oracle("W9E1", BUNNY_CAM, W, H, (int(x), int(y), 1, 1), 0, 256)
         assert np.array_equal(_bits(full[0][y, x]), _bits(o[0][0, 0])), (x, y, full[0][y, x], o[0][0, 0])
         assert full[1][y, x] == o[1][0, 0]
+
+
+def test_config3_full_frame_baseline_spp_equals_oracle(rt, bunny):
+    # the headline frame whole, not by transitivity through the
+    # unculled walk -- every one of its 530.8 M samples, in one launch
+    assert rt._ffi.RT_BSP_CULL_CERTIFIED == 1
+    # (the bench's own kernel instantiation: no counting build; that culling is
+    # active on this frame is test_gpu_cull_fullframe.py's business)
+    bunny.ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, rt._ffi.RT_BSP_CULL_CERTIFIED)
+    g = bunny.render_gpu("W9E1", BUNNY_CAM, W, H, (0, 0, W, H), 0, 256)
+    assert g[2]["samples"] == W * H * 256
+    o = bunny.render_oracle("W9E1", BUNNY_CAM, W, H, (0, 0, W, H), 0, 256)
+    check(g, o)
 
 
 def test_config3_eight_rank_tiles_equal_frame(rt, bunny):

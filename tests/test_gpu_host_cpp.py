@@ -108,9 +108,13 @@ def test_tiled_one_rank_communicator_equals_plain_frame(rt, tmp_path, scene, arg
     # (rt_comm_unique_id published in a file, rt_comm_init, rt_gather_tiles):
     # the frame equals the plain region render's bit for bit
     plain = cpp_render(tmp_path, scene, 72, 40, *args)
+    # a file left by an earlier launch (another token) is replaced, never used
+    (tmp_path / "comm.id").write_bytes(b"RTCOMMID old-launch\n" + bytes(128))
     tiled = cpp_render(tmp_path, scene, 72, 40, *args, "--nranks", "1", "--rank", "0", "--comm-file",
-                       str(tmp_path / "comm.id"))
-    assert os.path.getsize(tmp_path / "comm.id") == 128
+                       str(tmp_path / "comm.id"), "--comm-token", "job-42")
+    blob = (tmp_path / "comm.id").read_bytes()
+    assert blob.startswith(b"RTCOMMID job-42\n") and len(blob) == len(b"RTCOMMID job-42\n") + 128
+    assert blob[-128:] != bytes(128)
     for a, b in zip(plain[:3], tiled[:3]):
         assert np.array_equal(a.view(np.uint32) if a.dtype == np.float32 else a,
                               b.view(np.uint32) if b.dtype == np.float32 else b)

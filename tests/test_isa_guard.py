@@ -55,11 +55,13 @@ WHOLE_BUDGET = {
     # margin) and the 96-B treelets a sixth load: 104/90 and 64/59 (from 72/67, 44/43);
     # the camera bound (eye compare, |w|inf, the eye term) 108/93 and 68/58; its
     # per-treelet precomputed form 108/93 and 64/56.
-    "k_pathILi4ELi0ELb0ELb1": (108, 93),    # W9E1, BSP
+    # round 5: the zero-component slab of the cull (an infinite reciprocal, the
+    # capped gap tolerance) and bsp_inv1's flag: 108/99, and W7E3 72/62 / 64/56.
+    "k_pathILi4ELi0ELb0ELb1": (108, 99),    # W9E1, BSP
     "k_pathILi4ELi0ELb0ELb0": (88, 99),     # W9E1, BSP, the fast-margin instantiation
     "k_pathILi4ELi1ELb0ELb1": (80, 77),     # W9E1, BVH
-    "k_pathILi3ELi0ELb0ELb1": (64, 56),
-    "k_pathILi3ELi0ELb0ELb0": (68, 63),     # W7E3, BSP, the fast-margin instantiation     # W7E3, BSP at 7 waves/SIMD (0/0 at 5)
+    "k_pathILi3ELi0ELb0ELb1": (72, 62),     # W7E3, BSP at 7 waves/SIMD
+    "k_pathILi3ELi0ELb0ELb0": (64, 56),     # W7E3, BSP, the fast-margin instantiation (0/0 at 5)
 }
 
 

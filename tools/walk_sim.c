@@ -68,7 +68,11 @@ int g_bad_n = 0;
 int walk_sim_bad(double* out) { for (int i = 0; i < 4 * g_bad_n; i++) out[i] = g_bad[i]; return g_bad_n; }
 double g_cull[32], g_cull_leaf;
 void walk_sim_culls(double* out) { for (int i = 0; i < 32; i++) out[i] = g_cull[i]; out[32] = g_cull_leaf; }
-void walk_sim_root_only(int r) { g_root_only = r; }   /* nnodes x 6: content box (min.xyz, max.xyz) of each node's subtree, or NULL */
+void walk_sim_root_only(int r) { g_root_only = r; }
+/* WALK_AXIS: 1 (default) an axis with |d| < 1e-8 culls on the origin's coordinate
+ * against the grown box (option (a)); 0 it constrains nothing (round 4's kernel) */
+int g_axis = 1;
+void walk_sim_axis(int a) { g_axis = a; }   /* nnodes x 6: content box (min.xyz, max.xyz) of each node's subtree, or NULL */
 void walk_sim_boxes(const float* b) { g_boxes = b; }
 static float g_tn, g_tf;   /* the ray interval clipped to the last tested box */
 /* WALK_CERT: the certified margin (DESIGN.md section 4 "Certified culling"):
@@ -85,10 +89,67 @@ static int g_cert_is_floor = 0;
  * camera eye E (camera rays start at E: the accept point must then be near the plane of
  * the triangle *and* the eye off it, which bounds |denom| below) */
 static const double* g_hcam = 0;
+/* WALK_SHADOW: per node min over the subtree's triangles of |n*_y| / E_T^2 (option (b):
+ * the W9E1 shadow direction (0, 1, 0) is fixed, so |w . n*| is known per treelet) */
+static const double* g_hy = 0;
+void walk_sim_hy(const double* h) { g_hy = h; }
 static v3 g_eye;
 void walk_sim_cam(const double* h, float ex, float ey, float ez) { g_hcam = h; g_eye = V(ex, ey, ez); }
 double g_lost[4];
 void walk_sim_lost(double* o) { for (int i = 0; i < 4; i++) o[i] = g_lost[i]; }
+/* WALK_CAMX=k: the camera term over each subtree with its k triangles of smallest H
+ * (the eye's distance from their planes) left out; a camera-ray cull that only those
+ * triangles prevent tests them directly with the ray's interval (a second load and
+ * up to k tests) and culls when none is accepted -- exact by the same argument */
+static int g_camx = 0, g_use_hx = 0;
+static double* g_hx = 0;     /* per node: the (k+1)-th smallest H of the subtree */
+static uint32_t* g_xt = 0;   /* per node: its k excluded triangles (~0u: none) */
+static const uint32_t* g_tree_x = 0;
+static const uint32_t* g_ids_x = 0;
+static const double* g_htri = 0;
+double g_camx_stat[4];   /* culls won, excluded-triangle tests, won culls refused by an accept, checks */
+void walk_sim_camx_stats(double* o) { for (int i = 0; i < 4; i++) o[i] = g_camx_stat[i]; }
+#define CAMX_MAX 8
+typedef struct { int n; double h[CAMX_MAX + 1]; uint32_t t[CAMX_MAX + 1]; } XList;
+static void xl_add(XList* l, double h, uint32_t t, int cap)
+{
+    for (int i = 0; i < l->n; i++) if (l->t[i] == t) return;
+    int i;
+    if (l->n < cap) i = l->n++;
+    else if (h >= l->h[cap - 1]) return;
+    else i = cap - 1;
+    l->h[i] = h; l->t[i] = t;
+    while (i > 0 && l->h[i] < l->h[i - 1]) {
+        double th = l->h[i]; l->h[i] = l->h[i - 1]; l->h[i - 1] = th;
+        uint32_t tt = l->t[i]; l->t[i] = l->t[i - 1]; l->t[i - 1] = tt;
+        i--;
+    }
+}
+static XList camx_rec(uint32_t node, uint32_t nnodes)
+{
+    XList l; l.n = 0;
+    const int cap = g_camx + 1;
+    if (node >= nnodes) return l;
+    const uint32_t* tn = g_tree_x + 4 * (size_t)node;
+    if ((tn[0] & 3u) == 3u) {
+        for (uint32_t j = 0; j < (tn[0] >> 2); j++) xl_add(&l, g_htri[g_ids_x[tn[1] + j]], g_ids_x[tn[1] + j], cap);
+    } else {
+        XList a = camx_rec(2 * node + 1, nnodes), b = camx_rec(2 * node + 2, nnodes);
+        for (int i = 0; i < a.n; i++) xl_add(&l, a.h[i], a.t[i], cap);
+        for (int i = 0; i < b.n; i++) xl_add(&l, b.h[i], b.t[i], cap);
+    }
+    g_hx[node] = l.n > g_camx ? l.h[g_camx] : INFINITY;
+    for (int i = 0; i < g_camx; i++) g_xt[(size_t)node * CAMX_MAX + i] = i < l.n ? l.t[i] : ~0u;
+    return l;
+}
+void walk_sim_camx(const uint32_t* tree, const uint32_t* ids, uint32_t nnodes, const double* htri, int k)
+{
+    g_camx = k > CAMX_MAX ? CAMX_MAX : k;
+    g_tree_x = tree; g_ids_x = ids; g_htri = htri;
+    g_hx = (double*)malloc(sizeof(double) * nnodes);
+    g_xt = (uint32_t*)malloc(sizeof(uint32_t) * CAMX_MAX * (size_t)nnodes);
+    camx_rec(0, nnodes);
+}
 static double cert_margin_c(const double* c, v3 o, v3 d, const float* b);
 static double cert_margin(uint32_t node, v3 o, v3 d, const float* b) { return cert_margin_c(g_cert + 7 * (size_t)node, o, d, b); }
 static double cert_margin_c(const double* c, v3 o, v3 d, const float* b)
@@ -118,9 +179,14 @@ static double cert_margin_c(const double* c, v3 o, v3 d, const float* b)
             double a = fabs(b[k] - comp(o, k)), e = fabs(b[3 + k] - comp(o, k));
             Dinf = fmax(Dinf, fmax(a, e));
         }
-        double H = g_hcam[c - g_cert >= 0 && (c - g_cert) % 7 == 0 ? (c - g_cert) / 7 : 0];
+        const size_t nd = c - g_cert >= 0 && (c - g_cert) % 7 == 0 ? (c - g_cert) / 7 : 0;
+        double H = g_use_hx ? g_hx[nd] : g_hcam[nd];
         double dc = winf * (H - 128 * u * d1) / Dinf;
         if (dc > den) den = dc;
+    }
+    if (g_hy && d.x == 0.0f && d.y == 1.0f && d.z == 0.0f) {
+        const double hy = g_hy[(c - g_cert) / 7] - 20 * u;
+        if (hy > den) den = hy;
     }
     if (g_cert_floor_only == 2) return 1e30;
     g_cert_is_floor = den == fl;
@@ -153,6 +219,7 @@ static int cell_clip(uint32_t node, v3 o, v3 d, double* t0p, double* t1p)
     *t1p = t1;
     return t0 > t1 + (fabs(t0) + fabs(t1)) * 0x1p-18;
 }
+static const Scene* g_scene = 0;
 static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
 {
     const float* b = g_boxes + 6 * (size_t)node;
@@ -168,7 +235,7 @@ static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
         double t0 = tmin, t1 = tmax;
         for (int k = 0; k < 3; k++) {
             double dk = comp(d, k), ok = comp(o, k);
-            if (fabs(dk) < 1e-8) { if (ok < b[k] - m || ok > b[3 + k] + m) return 1; continue; }
+            if (fabs(dk) < 1e-8) { if (g_axis && dk == 0.0f && (ok < b[k] - m || ok > b[3 + k] + m)) return 1; continue; }
             double a = (b[k] - m - ok) / dk, cc = (b[3 + k] + m - ok) / dk;
             if (a > cc) { double x = a; a = cc; cc = x; }
             if (a > t0) t0 = a;
@@ -177,6 +244,33 @@ static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
         g_tn = (float)t0;
         g_tf = (float)t1;
         int miss = t0 > t1 + (fabs(t0) + fabs(t1)) * 0x1p-18;
+        if (!miss && g_camx && g_hcam && o.x == g_eye.x && o.y == g_eye.y && o.z == g_eye.z && isfinite(g_hx[node])) {
+            g_use_hx = 1;
+            const double m2 = cert_margin(node, o, d, b);
+            g_use_hx = 0;
+            double a0 = tmin, a1 = tmax;
+            for (int k = 0; k < 3; k++) {
+                double dk = comp(d, k), ok = comp(o, k);
+                if (fabs(dk) < 1e-8) { if (g_axis && dk == 0.0f && (ok < b[k] - m2 || ok > b[3 + k] + m2)) { a0 = 1; a1 = 0; } continue; }
+                double a = (b[k] - m2 - ok) / dk, cc = (b[3 + k] + m2 - ok) / dk;
+                if (a > cc) { double x = a; a = cc; cc = x; }
+                if (a > a0) a0 = a;
+                if (cc < a1) a1 = cc;
+            }
+            g_camx_stat[3] += 1;
+            if (a0 > a1 + (fabs(a0) + fabs(a1)) * 0x1p-18) {
+                int acc = 0;
+                for (int j = 0; j < g_camx; j++) {
+                    uint32_t t = g_xt[(size_t)node * CAMX_MAX + j];
+                    if (t == ~0u) continue;
+                    float dd;
+                    g_camx_stat[1] += 1;
+                    if (tri(g_scene, t, o, d, tmin, tmax, &dd)) { acc = 1; break; }
+                }
+                if (!acc) { g_camx_stat[0] += 1; return 1; }
+                g_camx_stat[2] += 1;
+            }
+        }
         if (!miss) {
             /* would the fast margin (2^-10 of max(|o|, scene)) have culled? */
             double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));
@@ -386,6 +480,7 @@ int walk_sim(const uint32_t* tree, const float* planes, const uint32_t* ids, con
              const float* rays, const uint32_t* flags, uint32_t n, double* out)
 {
     Scene s = {tree, planes, ids, pos, idx};
+    g_scene = &s;
     memset(out, 0, sizeof(double) * 5 * S_N);
     for (uint32_t i = 0; i < n; i++) {
         const float* r = rays + 8 * (size_t)i;

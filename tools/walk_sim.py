@@ -202,6 +202,12 @@ def main():
         L.walk_sim_cert(cert.ctypes.data, float(np.abs(pos[:, :3]).max()), int(os.environ.get("WALK_CERT_FLOOR", "0")))
         if os.environ.get("WALK_CELLS"):
             L.walk_sim_cells(P(occ.ctypes.data))
+        if os.environ.get("WALK_SHADOW"):
+            hy = np.full(n, np.inf)
+            hy[lv] = leaf_reduce(np.abs(nst[:, 1]), np.minimum)
+            up(hy, np.minimum)
+            hy = np.ascontiguousarray(np.where(np.isfinite(hy), hy / cert[:, 0], 0.0))
+            L.walk_sim_hy(P(hy.ctypes.data))
         if os.environ.get("WALK_CAM"):
             eye = np.asarray(cfg.camera[0], np.float32)
             hn = np.abs(((v0.astype(np.float64) - eye.astype(np.float64)) * nst).sum(1)) / np.maximum(Et2, 1e-300)
@@ -209,9 +215,14 @@ def main():
             hcam[lv] = leaf_reduce(hn, np.minimum)
             up(hcam, np.minimum)
             hcam = np.ascontiguousarray(hcam)
+            if os.environ.get("WALK_CAMX"):
+                hn_c = np.ascontiguousarray(hn)
+                L.walk_sim_camx(P(tree.ctypes.data), P(ids.ctypes.data), ctypes.c_uint32(n), P(hn_c.ctypes.data),
+                                int(os.environ["WALK_CAMX"]))
             L.walk_sim_cam.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
             L.walk_sim_cam(hcam.ctypes.data, *[float(x) for x in eye])
     L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
+    L.walk_sim_axis(int(os.environ.get("WALK_AXIS", "1")))
     L.walk_sim_cull_every(int(os.environ.get("WALK_CULL_EVERY", "0")))
     L.walk_sim_clip(int(os.environ.get("WALK_CLIP", "0")))
     L.walk_sim_chunk.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float]
@@ -252,6 +263,11 @@ def main():
         lo_ = np.zeros(4)
         L.walk_sim_lost(P(lo_.ctypes.data))
         print("fast culls lost by the certified test per ray: cone regime %.3f, floor regime %.3f" % (lo_[0] / len(R), lo_[1] / len(R)))
+        if os.environ.get("WALK_CAMX"):
+            cx = np.zeros(4)
+            L.walk_sim_camx_stats(P(cx.ctypes.data))
+            print("camx per ray: culls won %.3f, excluded-triangle tests %.3f, refused %.4f, checks %.3f"
+                  % tuple(v / len(R) for v in cx))
     print(f"config {cfgn}: {len(R)} rays ({sum(flags)} any-hit), {time.time() - t0:.1f} s")
     for v in range(5 if boxes is not None else 3):
         s = {k: round(out[v, i] / len(R), 3) for i, k in enumerate(NAMES)}
