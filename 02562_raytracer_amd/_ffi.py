@@ -33,7 +33,8 @@ RT_OPT_SAMPLE_BUDGET_MB = 5
 RT_OPT_UNIT_ORDER = 6
 RT_OPT_BSP_CULL = 9
 RT_OPT_ASYNC_FOLD = 10
-RT_BSP_CULL_OFF, RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_FAST = range(3)
+RT_BSP_CULL_OFF, RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_FAST, RT_BSP_CULL_SILHOUETTE = range(4)
+BSP_TREELET_BYTES = 96   # rt_internal.h: the BSP walk's treelet (rt_download_bsp_treelets)
 RT_OPT_KERNEL_TIMING = 7
 RT_COMM_ID_BYTES = 128
 
@@ -165,6 +166,9 @@ SIGNATURES = {
     "rt_comm_destroy": (C.c_int, [vp]),
     "rt_gather_tiles": (C.c_int, [vp, C.c_uint32, C.c_uint32, vp, vp, vp, vp]),
     "rt_trace_rays": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp]),
+    "rt_trace_batch": (C.c_int, [vp, C.c_int, vp, vp, C.c_uint32, vp]),
+    "rt_set_ray_capture": (C.c_int, [vp, vp, vp, C.c_uint64]),
+    "rt_ray_capture_count": (C.c_int, [vp, C.POINTER(C.c_uint64)]),
     "rt_last_counts": (C.c_int, [vp, C.POINTER(RayCounts)]),
     "rt_selftest_math": (C.c_int, [vp, C.c_uint32, C.c_float, C.c_float, u32p]),
     "rt_mesh_load_obj": (C.c_int, [C.c_char_p, C.POINTER(vp)]),

@@ -299,14 +299,18 @@ class Context:
                                           aabb.ctypes.data_as(F.f32p), C.byref(nn), C.byref(ni)))
         return tree[:nn.value], planes[:nn.value], ids[:ni.value], aabb
 
-    def download_bsp_treelets(self):
+    def download_bsp_treelets(self, silhouette=False):
         """The BSP walk's 96-B treelets as u32[nnodes + 1, 24] (rt_download_bsp_treelets;
-        diagnostics: the certified culling's per-subtree data)."""
+        diagnostics: the certified culling's per-subtree data); with silhouette=True
+        also RT_BSP_CULL_SILHOUETTE's node data as u32[nnodes + 1, 4]."""
         nb = C.c_uint64()
         self._chk(F.lib().rt_download_bsp_treelets(self._h, None, 0, C.byref(nb)))
         out = np.zeros(nb.value // 4, np.uint32)
         self._chk(F.lib().rt_download_bsp_treelets(self._h, out.ctypes.data_as(C.c_void_p), nb.value, C.byref(nb)))
-        return out.reshape(-1, 24)
+        w = F.BSP_TREELET_BYTES // 4
+        slots = out.size // (w + 4)
+        tl = out[:slots * w].reshape(-1, w)
+        return (tl, out[slots * w:].reshape(-1, 4)) if silhouette else tl
 
     def download_bvh(self):
         """(nodes[n,8] u32 view of GpuNode, tri_ids[k] u32) of this context's BVH."""
@@ -467,6 +471,22 @@ class Context:
         n = C.c_uint32()
         self._chk(F.lib().rt_kernel_time(self._h, int(reset), C.byref(ms), C.byref(n)))
         return ms.value, n.value
+
+    def trace_batch(self, trav, rays_ptr, flags_ptr, n, hits_ptr):
+        """rt_trace_batch: the traversal-only kernel over n device rays (8 f32 each;
+        flags bit 0 any-hit, or None) into n x {record offset | 0xFFFFFFFE | ~0, dist}."""
+        self._chk(F.lib().rt_trace_batch(self._h, F.TRAVERSALS.get(trav, trav), C.c_void_p(rays_ptr),
+                                          C.c_void_p(flags_ptr) if flags_ptr else None, n, C.c_void_p(hits_ptr)))
+
+    def set_ray_capture(self, rays_ptr=None, flags_ptr=None, cap=0):
+        """Arm (device buffers of cap rays) or disarm (None) the counting renders' ray capture."""
+        self._chk(F.lib().rt_set_ray_capture(self._h, C.c_void_p(rays_ptr) if rays_ptr else None,
+                                              C.c_void_p(flags_ptr) if flags_ptr else None, cap))
+
+    def ray_capture_count(self):
+        n = C.c_uint64()
+        self._chk(F.lib().rt_ray_capture_count(self._h, C.byref(n)))
+        return n.value
 
     def gather_time(self, reset=True):
         """(transfer ms, unpack ms, calls) of the frame assembly timed since the last

@@ -84,6 +84,7 @@ struct rt_ctx {
     bool has_mesh = false;
     DevBuf pos, nrm, idx, mats, lights;
     DevBuf bsp_nodes, bsp_ids;   // bsp_nodes: [8-B nodes | 48-B records]
+    DevBuf bsp_tm;               // per record slot {triangle id, material} (DevScene.bsp_tm)
     DevBuf bsp_ref_tree, bsp_ref_planes;   // bsp_array + planes in the reference layout (rt_download_bsp)
     float bsp_aabb8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t bsp_nnodes = 0, bsp_nids = 0;
@@ -95,6 +96,7 @@ struct rt_ctx {
     bool hcam_valid = false;
     float hcam_eye[3] = {0, 0, 0};
     DevBuf hcam_scratch;
+    DevBuf bsp_sil;   // RT_BSP_CULL_SILHOUETTE's node data ((nnodes + 1) x 16 B)
     DevBuf bvh_nodes, bvh_ids;   // bvh_nodes: [32-B nodes | 48-B records]
     DevBuf bvh_ref;              // the GpuNode array in the reference layout (rt_download_bvh)
     uint32_t bvh_rec_off = 0;
@@ -130,6 +132,11 @@ struct rt_ctx {
     DevBuf samples2;
     uint32_t sbuf = 0;
     bool fold_pending = false;   // work on fold_stream the context stream has not joined yet
+    // rt_set_ray_capture: the counting renders append their traced rays here (device)
+    float* cap_rays = nullptr;
+    uint32_t* cap_flags = nullptr;
+    uint64_t cap_max = 0;
+    DevBuf cap_count;
     ncclComm_t comm = nullptr;
     uint32_t comm_nranks = 0, comm_rank = 0;
     DevBuf gather_accum, gather_ids;   // rank 0: every rank's packed tiles, rank-major
@@ -342,8 +349,8 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
         c->ktiming = value != 0;
         return RT_OK;
     case RT_OPT_BSP_CULL:
-        if (value < RT_BSP_CULL_OFF || value > RT_BSP_CULL_FAST)
-            return fail(c, RT_E_INVALID, "BSP cull must be RT_BSP_CULL_OFF, _CERTIFIED or _FAST");
+        if (value < RT_BSP_CULL_OFF || value > RT_BSP_CULL_SILHOUETTE)
+            return fail(c, RT_E_INVALID, "BSP cull must be RT_BSP_CULL_OFF, _CERTIFIED, _FAST or _SILHOUETTE");
         c->bsp_cull = (uint32_t)value;
         return RT_OK;
     case RT_OPT_UNIT_ORDER:
@@ -501,7 +508,7 @@ int rt_upload_mesh(rt_ctx* c, const float* pos_vec4, const float* nrm_vec4, uint
 
 // The traversal layout of the context's BSP (reference arrays already in
 // bsp_ref_tree / bsp_ref_planes / bsp_ids, mesh in pos / idx): content boxes,
-// 80-B treelets and the 48-B records (rt_bsp_build.hip launch_bsp_repack), and
+// 96-B treelets and the 48-B records (rt_bsp_build.hip launch_bsp_repack), and
 // the scale of the content boxes' margins: the largest coordinate magnitude of
 // the BSP's root box (bsp_box_miss in rt_kernels.hip adds the ray origin's).
 static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off, size_t total, const float aabb[8])
@@ -510,9 +517,10 @@ static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off,
     HIPCHK(c, c->bsp_nodes.alloc(total));
     DevBuf boxes;
     HIPCHK(c, boxes.alloc((size_t)nnodes * 64));
+    HIPCHK(c, c->bsp_tm.alloc((size_t)std::max<uint32_t>(nids, 1u) * 8));
     if (rtk::launch_bsp_repack(c->bsp_ref_tree.as<uint32_t>(), c->bsp_ref_planes.as<float>(), nnodes,
                                (uint32_t)rec_off, c->bsp_nodes.p, c->pos.as<float4>(), c->idx.as<uint4>(),
-                               c->bsp_ids.as<uint32_t>(), nids, 0.0f, boxes.p, c->stream))
+                               c->bsp_ids.as<uint32_t>(), nids, 0.0f, boxes.p, c->bsp_tm.as<uint2>(), c->stream))
         return fail(c, RT_E_DEVICE, "BSP repack launch failed");
     HIPCHK(c, hipStreamSynchronize(c->stream));
     float scale = 0.0f;
@@ -763,13 +771,18 @@ int rt_download_bsp_treelets(rt_ctx* c, void* dst, uint64_t cap_bytes, uint64_t*
 {
     if (!c) return RT_E_INVALID;
     if (!c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_download_bsp_treelets: no BSP on the context");
-    const uint64_t n = ((uint64_t)c->bsp_nnodes + 1) * rtk::BSP_TREELET_BYTES;
+    const uint64_t nt = ((uint64_t)c->bsp_nnodes + 1) * rtk::BSP_TREELET_BYTES;
+    const uint64_t ns = ((uint64_t)c->bsp_nnodes + 1) * 16;
+    const uint64_t n = nt + ns;
     if (bytes) *bytes = n;
     if (!dst) return RT_OK;
     if (cap_bytes < n) return fail(c, RT_E_INVALID, "rt_download_bsp_treelets: buffer too small");
     if (int r = set_dev(c)) return r;   // (first: ensure_hcam may launch the camera-term kernels)
     if (int r = ensure_hcam(c)) return r;
-    HIPCHK(c, hipMemcpyAsync(dst, c->bsp_nodes.p, n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dst, c->bsp_nodes.p, nt, hipMemcpyDeviceToHost, c->stream));
+    if (c->bsp_sil.n >= ns) HIPCHK(c, hipMemcpyAsync(static_cast<uint8_t*>(dst) + nt, c->bsp_sil.p, ns,
+                                                     hipMemcpyDeviceToHost, c->stream));
+    else memset(static_cast<uint8_t*>(dst) + nt, 0, ns);
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return RT_OK;
 }
@@ -892,13 +905,17 @@ int rt_set_environment_map(rt_ctx* c, const uint8_t* rgba8, uint32_t width, uint
 // rt_bsp_build.hip launch_bsp_camera): recomputed when the eye moves.
 static int ensure_hcam(rt_ctx* c)
 {
-    if (!c->has_bsp || !c->has_u || c->bsp_cull != RT_BSP_CULL_CERTIFIED) return RT_OK;
+    if (!c->has_bsp || !c->has_u || (c->bsp_cull != RT_BSP_CULL_CERTIFIED && c->bsp_cull != RT_BSP_CULL_SILHOUETTE))
+        return RT_OK;
     const float* e = c->u.camera_pos;
     if (c->hcam_valid && memcmp(e, c->hcam_eye, sizeof c->hcam_eye) == 0) return RT_OK;
     if (!(std::isfinite(e[0]) && std::isfinite(e[1]) && std::isfinite(e[2]))) return RT_OK;
-    HIPCHK(c, c->hcam_scratch.ensure((size_t)c->bsp_nnodes * 4));
+    HIPCHK(c, c->hcam_scratch.ensure((size_t)c->bsp_nnodes * 24));
+    HIPCHK(c, c->bsp_sil.ensure(((size_t)c->bsp_nnodes + 1) * 16));
+    HIPCHK(c, hipMemsetAsync(c->bsp_sil.p, 0, 16, c->stream));   // (slot 0: no node)
     if (rtk::launch_bsp_camera(c->bsp_ref_tree.as<uint32_t>(), c->bsp_nnodes, c->pos.as<float4>(), c->idx.as<uint4>(),
-                               c->bsp_ids.as<uint32_t>(), c->bsp_nids, e, c->bsp_nodes.p, c->hcam_scratch.p, c->stream))
+                               c->bsp_ids.as<uint32_t>(), c->bsp_nids, e, c->bsp_nodes.p, c->bsp_sil.as<uint32_t>(),
+                               c->hcam_scratch.p, c->stream))
         return fail(c, RT_E_DEVICE, "BSP camera terms: launch failed");
     memcpy(c->hcam_eye, e, sizeof c->hcam_eye);
     c->hcam_valid = true;
@@ -924,6 +941,12 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bsp_bytes = (uint32_t)c->bsp_nodes.n;
     S.bsp_rec_off = c->bsp_rec_off;
     S.bsp_ids = c->bsp_ids.as<uint32_t>();
+    S.bsp_tm = c->bsp_tm.as<uint2>();
+    S.bsp_sil = c->bsp_sil.as<uint4>();
+    // the silhouette mode needs its node data, made with the camera terms (ensure_hcam);
+    // without them (no uniforms, or a non-finite eye) it runs the certified kernel
+    S.bsp_cull_mode = c->bsp_cull == RT_BSP_CULL_SILHOUETTE && !c->hcam_valid ? (uint32_t)RT_BSP_CULL_CERTIFIED
+                                                                                : (uint32_t)c->bsp_cull;
     S.bsp_depth = c->bsp_depth;
     memcpy(S.aabb, c->aabb, sizeof S.aabb);
     S.bvh_base = c->bvh_nodes.as<uint8_t>();
@@ -936,7 +959,7 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bsp_cull_emax = c->bsp_cull != RT_BSP_CULL_OFF ? FLT_MAX : INFINITY;
     // off: the fast formula's constants (k1 = 0 picks k_path's fast-margin
     // instantiation, launch_path); the +inf gap culls nothing either way
-    if (c->bsp_cull != RT_BSP_CULL_CERTIFIED) {
+    if (c->bsp_cull != RT_BSP_CULL_CERTIFIED && c->bsp_cull != RT_BSP_CULL_SILHOUETTE) {
         S.cull_k1 = 0.0f;
         S.cull_k3 = 0.0f;
         S.cull_ko = 0x1p-10f;
@@ -948,6 +971,59 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
         S.bsp_margin = std::ldexp(c->bsp_scale, -19);
     }
     return S;
+}
+
+int rt_set_ray_capture(rt_ctx* c, float* rays_dev, uint32_t* flags_dev, uint64_t cap)
+{
+    if (!c || (rays_dev && !flags_dev)) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    if (rays_dev && !c->cap_count.p) HIPCHK(c, c->cap_count.alloc(8));
+    if (rays_dev) HIPCHK(c, hipMemsetAsync(c->cap_count.p, 0, 8, c->stream));
+    c->cap_rays = rays_dev;
+    c->cap_flags = flags_dev;
+    c->cap_max = rays_dev ? cap : 0;
+    return RT_OK;
+}
+
+int rt_ray_capture_count(rt_ctx* c, uint64_t* n)
+{
+    if (!c || !n) return RT_E_INVALID;
+    if (int r = set_dev(c)) return r;
+    *n = 0;
+    if (!c->cap_count.p) return RT_OK;
+    HIPCHK(c, hipMemcpyAsync(n, c->cap_count.p, 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return RT_OK;
+}
+
+int rt_trace_batch(rt_ctx* c, rt_traverse trav, const float* rays_dev, const uint32_t* flags_dev, uint32_t n,
+                   uint32_t* hits_dev)
+{
+    if (!c) return RT_E_INVALID;
+    if (n == 0) return RT_OK;
+    if (!rays_dev || !hits_dev) return fail(c, RT_E_INVALID, "rt_trace_batch: rays and hits are required");
+    if (trav != RT_TRAVERSE_BSP) return fail(c, RT_E_UNSUPPORTED, "rt_trace_batch: the BSP walk only");
+    if (!c->has_mesh || !c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_trace_batch: no BSP uploaded");
+    if (int r = set_dev(c)) return r;
+    if (int r = ensure_hcam(c)) return r;
+    const uint32_t T = c->shade_threshold >= 0 ? (uint32_t)c->shade_threshold & 0xFFu : 16u;
+    const bool t = c->ktiming && c->kused + 2 <= 8192;
+    if (t) {
+        while (c->kev.size() < c->kused + 2) {
+            hipEvent_t e;
+            HIPCHK(c, hipEventCreate(&e));
+            c->kev.push_back(e);
+        }
+        HIPCHK(c, hipEventRecord(c->kev[c->kused], c->stream));
+    }
+    const int r = rtk::launch_trace_batch(dev_scene(c), rays_dev, flags_dev, n, hits_dev, c->work.as<uint32_t>(),
+                                          T < 64u ? T : 63u, c->num_cus, c->stream);
+    if (r) return fail(c, r, std::string("rt_trace_batch: launch failed: ") + hipGetErrorString(hipGetLastError()));
+    if (t) {
+        HIPCHK(c, hipEventRecord(c->kev[c->kused + 1], c->stream));
+        c->kused += 2;
+    }
+    return RT_OK;
 }
 
 int rt_trace_rays(rt_ctx* c, rt_traverse trav, const float* rays, const uint32_t* flags, uint32_t n, rt_ray_hit* hits)
@@ -1010,6 +1086,10 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     L.env_w = c->env_w;
     L.env_h = c->env_h;
     L.work_counter = c->work.as<uint32_t>();
+    L.cap_rays = reinterpret_cast<float4*>(c->cap_rays);
+    L.cap_flags = c->cap_flags;
+    L.cap_count = c->cap_count.as<unsigned long long>();
+    L.cap_max = c->cap_max;
     if (trav == RT_TRAVERSE_BVH) {
         const size_t need = rtk::bvh_deep_bytes(c->num_cus, c->waves_per_cu);
         if (c->bvh_deep.n < need) HIPCHK(c, c->bvh_deep.alloc(need));
@@ -1027,7 +1107,8 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // nodes and its rays take more trips, so finished lanes wait longer for the last
     // ones: 16 and 32 (profiles/r04/sweep_T.txt: config 3 fixed 16 +1.9 % over 8,
     // config 4 16..24 +3 %, config 5 32 +1.1 %).
-    const uint32_t adaptive = c->bsp_cull == RT_BSP_CULL_CERTIFIED ? (1u << 16) | (32u << 8) | 16u
+    const uint32_t adaptive = c->bsp_cull == RT_BSP_CULL_CERTIFIED || c->bsp_cull == RT_BSP_CULL_SILHOUETTE
+                                  ? (1u << 16) | (32u << 8) | 16u
                                                                    : (1u << 16) | (24u << 8) | 8u;
     L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold
                                    : trav == RT_TRAVERSE_BVH ? 4

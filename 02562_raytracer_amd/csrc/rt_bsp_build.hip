@@ -523,7 +523,7 @@ __device__ __forceinline__ uint32_t h_ru(float x) { return __half_as_ushort(__fl
 
 // The 96-B treelet of 1-based node M at 96*M (rt_internal.h BSP_TREELET_BYTES):
 // {box min.xyz, max.x | max.y, max.z, node M | nodes 2M, 2M+1 | 4M, 4M+1 |
-//  4M+2, 4M+3 | F, c.xy, c.z r.x, r.yz}
+//  4M+2, 4M+3 | F G, c.xy, c.z r.x, r.yz}
 // -- node M's content box, expanded by `margin` on every side, the 8-B nodes a
 // three-level walk from M reads (interior {axis, plane bits}; leaf {3 |
 // (48*count) << 2, byte offset of its first record}), and the certification
@@ -587,11 +587,15 @@ __global__ void __launch_bounds__(256) k_bsp_repack(const uint32_t* tree, const 
     }
 }
 
+// The 48-B triangle records in treeIds order, and beside them each slot's
+// {triangle id, material} (tm: what shading resolves a BSP hit to, one load
+// instead of treeIds -> tri_idx; rt_kernels.hip resolve)
 __global__ void __launch_bounds__(256) k_tri_records2(const float4* pos, const uint4* idx, const uint32_t* ids,
-                                                      uint32_t nids, float4* recs)
+                                                      uint32_t nids, float4* recs, uint2* tm)
 {
     for (uint32_t k = blockIdx.x * 256u + threadIdx.x; k < nids; k += gridDim.x * 256u) {
         const uint4 ix = idx[ids[k]];
+        if (tm) tm[k] = make_uint2(ids[k], ix.w);
         const float4 a = pos[ix.x], b = pos[ix.y], c = pos[ix.z];
         const float e0[3] = {b.x - a.x, b.y - a.y, b.z - a.z};
         const float e1[3] = {c.x - a.x, c.y - a.y, c.z - a.z};
@@ -624,6 +628,46 @@ __device__ __forceinline__ float tri_hcam(const float4 v[3], const double E[3])
     if (!(eta > 0.0)) return 0.0f;
     return f_rd(eta / (Em * Em) * (1.0 - 0x1p-19));
 }
+// Per node, the three smallest H of its subtree with their triangles (distinct,
+// ascending; H = +inf / triangle ~0 where fewer): the camera term excludes the
+// first two (they are bounded per ray by their own normals instead) and takes
+// the third as the rest's minimum -- any other triangle's H is at least that.
+// Scratch: 6 words per node {h0, h1, h2, t0, t1, t2}.
+struct Top3 {
+    float h[3];
+    uint32_t t[3];
+};
+__device__ __forceinline__ void top3_add(Top3& a, float h, uint32_t t)
+{
+    if (t == ~0u) return;
+    for (int j = 0; j < 3; j++)
+        if (a.t[j] == t) return;   // (a triangle referenced by two leaves)
+    if (!(h < a.h[2])) return;
+    int j = 2;
+    while (j > 0 && h < a.h[j - 1]) {
+        a.h[j] = a.h[j - 1];
+        a.t[j] = a.t[j - 1];
+        j--;
+    }
+    a.h[j] = h;
+    a.t[j] = t;
+}
+__device__ __forceinline__ Top3 top3_load(const float* s, size_t i)
+{
+    Top3 a;
+    for (int j = 0; j < 3; j++) {
+        a.h[j] = s[6 * i + j];
+        a.t[j] = __float_as_uint(s[6 * i + 3 + j]);
+    }
+    return a;
+}
+__device__ __forceinline__ void top3_store(float* s, size_t i, const Top3& a)
+{
+    for (int j = 0; j < 3; j++) {
+        s[6 * i + j] = a.h[j];
+        s[6 * i + 3 + j] = __uint_as_float(a.t[j]);
+    }
+}
 __global__ void __launch_bounds__(256) k_leaf_hcam(const uint32_t* tree, uint32_t nnodes, const float4* pos,
                                                    const uint4* idx, const uint32_t* ids, uint32_t nids, double ex,
                                                    double ey, double ez, float* h)
@@ -631,15 +675,15 @@ __global__ void __launch_bounds__(256) k_leaf_hcam(const uint32_t* tree, uint32_
     const double E[3] = {ex, ey, ez};
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < nnodes; i += gridDim.x * 256u) {
         const uint32_t n0 = tree[4 * (size_t)i], first = tree[4 * (size_t)i + 1];
-        float m = INFINITY;
+        Top3 a = {{INFINITY, INFINITY, INFINITY}, {~0u, ~0u, ~0u}};
         const uint32_t cnt = (n0 & 3u) == 3u ? n0 >> 2 : 0u;
         if ((uint64_t)first + cnt <= nids)
             for (uint32_t k = 0; k < cnt; k++) {
                 const uint4 ix = idx[ids[first + k]];
                 const float4 v[3] = {pos[ix.x], pos[ix.y], pos[ix.z]};
-                m = fminf(m, tri_hcam(v, E));
+                top3_add(a, tri_hcam(v, E), ids[first + k]);
             }
-        h[i] = m;
+        top3_store(h, i, a);
     }
 }
 __global__ void __launch_bounds__(256) k_node_hcam(const uint32_t* tree, uint32_t nnodes, uint32_t lo_i, uint32_t hi_i,
@@ -647,8 +691,27 @@ __global__ void __launch_bounds__(256) k_node_hcam(const uint32_t* tree, uint32_
 {
     for (uint32_t i = lo_i + blockIdx.x * 256u + threadIdx.x; i < hi_i; i += gridDim.x * 256u) {
         if ((tree[4 * (size_t)i] & 3u) == 3u || 2ull * i + 2 >= nnodes) continue;
-        h[i] = fminf(h[2 * (size_t)i + 1], h[2 * (size_t)i + 2]);
+        Top3 a = top3_load(h, 2 * (size_t)i + 1);
+        const Top3 b = top3_load(h, 2 * (size_t)i + 2);
+        for (int j = 0; j < 3; j++) top3_add(a, b.h[j], b.t[j]);
+        top3_store(h, i, a);
     }
+}
+// n*/E_t^2 of triangle t (the records' f32 edges, the exact cross product in f64,
+// E_t its largest edge component) as three f16 rounded to nearest; NaN where the
+// triangle has no extent (it cannot be accepted: its denominator is 0)
+__device__ __forceinline__ void tri_nrm_h(const float4* pos, const uint4* idx, uint32_t t, uint32_t h[3])
+{
+    const uint4 ix = idx[t];
+    const float4 v[3] = {pos[ix.x], pos[ix.y], pos[ix.z]};
+    const float e0[3] = {v[1].x - v[0].x, v[1].y - v[0].y, v[1].z - v[0].z};
+    const float e1[3] = {v[2].x - v[0].x, v[2].y - v[0].y, v[2].z - v[0].z};
+    const double n[3] = {(double)e0[1] * e1[2] - (double)e0[2] * e1[1], (double)e0[2] * e1[0] - (double)e0[0] * e1[2],
+                         (double)e0[0] * e1[1] - (double)e0[1] * e1[0]};
+    const double Em = fmax(fmax(fmax(fabs((double)e0[0]), fabs((double)e0[1])), fabs((double)e0[2])),
+                           fmax(fmax(fabs((double)e1[0]), fabs((double)e1[1])), fabs((double)e1[2])));
+    for (int a = 0; a < 3; a++)
+        h[a] = Em > 0.0 ? __half_as_ushort(__float2half_rn((float)(n[a] / (Em * Em)))) : 0x7E00u;
 }
 // The camera term G of treelet M, into the high half of its q5.x as an f16
 // rounded down (G <= 2 sqrt(3): |n*| <= 2 E_T^2, |v0 - E| <= sqrt(3) Dinf): with D1 and Dinf the L1 and L-inf bounds of
@@ -656,8 +719,14 @@ __global__ void __launch_bounds__(256) k_node_hcam(const uint32_t* tree, uint32_
 // above, a camera ray's |denom| / E_T^2 >= ((H - 14u D1) |w|inf - 38u D1 |w|1) / Dinf
 // >= |w|inf (H - 128u D1) / Dinf = G |w|inf, since |w|1 <= 3 |w|inf (u = 2^-24;
 // the factor 1 - 2^-20 covers the kernel's one rounding of G |w|inf).
+// The silhouette data of RT_BSP_CULL_SILHOUETTE (16 B per 1-based node M in
+// `sil`): {x0.xy | x0.z x1.x | x1.yz | G_x}.  G_x, from the third smallest H, is
+// the camera bound for every triangle but the two excluded ones, whose normals
+// x = n*/E_t^2 (f16, nearest) the kernel dots with the ray:
+// |w . n*| / E_t^2 >= |w . x| - |w|1 (2 2^-11 + 2^-25 + 10u + rounding) >= |w . x| - 2^-9 |w|1
+// (|n*| / E_t^2 <= 2 per component; 10u: the test's own error of its denominator).
 __global__ void __launch_bounds__(256) k_treelet_hcam(const float* h, uint32_t nnodes, double ex, double ey, double ez,
-                                                      uint32_t* tl)
+                                                      const float4* pos, const uint4* idx, uint32_t* tl, uint32_t* sil)
 {
     constexpr uint32_t W = BSP_TREELET_BYTES / 4;
     const double E[3] = {ex, ey, ez};
@@ -671,15 +740,26 @@ __global__ void __launch_bounds__(256) k_treelet_hcam(const float* h, uint32_t n
         }
         D1 *= 1.0 + 0x1p-40;
         Dinf *= 1.0 + 0x1p-40;
-        const double H = h[m - 1];
-        float G = 0.0f;
-        if (H == INFINITY) G = INFINITY;   // no triangle of non-zero extent: F is +inf too
-        else if (Dinf > 0.0 && H - 128.0 * 0x1p-24 * D1 > 0.0) G = f_rd((H - 128.0 * 0x1p-24 * D1) / Dinf * (1.0 - 0x1p-20));
-        t[20] = (t[20] & 0xFFFFu) | (h_rd(G) << 16);
+        auto gterm = [&](double H) -> float {
+            if (H == INFINITY) return INFINITY;   // no triangle of non-zero extent: F is +inf too
+            if (Dinf > 0.0 && H - 128.0 * 0x1p-24 * D1 > 0.0) return f_rd((H - 128.0 * 0x1p-24 * D1) / Dinf * (1.0 - 0x1p-20));
+            return 0.0f;
+        };
+        const Top3 a = top3_load(h, m - 1);
+        t[20] = (t[20] & 0xFFFFu) | (h_rd(gterm(a.h[0])) << 16);
+        // the two excluded triangles (NaN slots: none) and the rest's term G_x
+        uint32_t x[6] = {0x7E00u, 0x7E00u, 0x7E00u, 0x7E00u, 0x7E00u, 0x7E00u};
+        for (int j = 0; j < 2; j++)
+            if (a.t[j] != ~0u && a.h[j] < INFINITY) tri_nrm_h(pos, idx, a.t[j], x + 3 * j);
+        uint32_t* q = sil + 4 * m;
+        q[0] = x[0] | (x[1] << 16);
+        q[1] = x[2] | (x[3] << 16);
+        q[2] = x[4] | (x[5] << 16);
+        q[3] = h_rd(gterm(a.h[2]));
     }
 }
 int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, const uint4* idx, const uint32_t* ids,
-                      uint32_t nids, const float eye[3], void* blob, void* scratch, hipStream_t s)
+                      uint32_t nids, const float eye[3], void* blob, uint32_t* sil, void* scratch, hipStream_t s)
 {
     float* h = reinterpret_cast<float*>(scratch);
     const uint32_t g0 = std::min<uint32_t>(16384, (nnodes + 255) / 256);
@@ -693,13 +773,13 @@ int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, 
         hipLaunchKernelGGL(k_node_hcam, dim3(g), dim3(256), 0, s, tree, nnodes, lo, hi, h);
     }
     hipLaunchKernelGGL(k_treelet_hcam, dim3(g0), dim3(256), 0, s, h, nnodes, (double)eye[0], (double)eye[1], (double)eye[2],
-                       reinterpret_cast<uint32_t*>(blob));
+                       pos, idx, reinterpret_cast<uint32_t*>(blob), sil);
     return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }
 
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
                       const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,
-                      void* box_scratch, hipStream_t s)
+                      void* box_scratch, uint2* tm, hipStream_t s)
 {
     // content boxes: leaves, then each depth bottom-up (depth d holds nodes [2^d - 1, 2^(d+1) - 1))
     float4* box = reinterpret_cast<float4*>(box_scratch);
@@ -719,7 +799,7 @@ int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes
     if (nids) {
         const uint32_t g2 = std::min<uint32_t>(16384, (nids + 255) / 256 + 1);
         hipLaunchKernelGGL(k_tri_records2, dim3(g2), dim3(256), 0, s, pos, idx, ids, nids,
-                           reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(blob) + rec_off));
+                           reinterpret_cast<float4*>(reinterpret_cast<uint8_t*>(blob) + rec_off), tm);
     }
     return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }

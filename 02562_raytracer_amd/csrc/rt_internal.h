@@ -57,6 +57,13 @@ struct DevScene {
     // origin coordinate lies outside the grown box) culls; +inf with culling off
     // (kept last: a field added mid-struct once moved the trip loop into spills)
     float bsp_cull_emax;
+    // per BSP record slot: {triangle id, material} (treeIds[k], tri_idx[treeIds[k]].w),
+    // so shading resolves a hit with one load (rt_kernels.hip resolve)
+    const uint2* bsp_tm;
+    // RT_BSP_CULL_SILHOUETTE: per 1-based node M, the camera term's two excluded
+    // triangles' normals and the rest's term, 16 B at [M] (rt_bsp_build.hip k_treelet_hcam)
+    const uint4* bsp_sil;
+    uint32_t bsp_cull_mode;   // RT_BSP_CULL_* (the host picks k_path's instantiation by it)
 };
 
 // Work mapping + outputs of one launch.
@@ -90,6 +97,13 @@ struct DevLaunch {
     uint32_t* work_counter;       // zeroed before launch
     unsigned long long* counters; // 32 x u64, zeroed before launch (rt_ray_counts order)
     uint32_t* bvh_deep;           // BVH stack entries beyond the LDS share: (50 - K) x grid lanes
+    // ray capture (rt_set_ray_capture; the counting instantiation only): every ray
+    // the path kernel's walks trace, appended as {o.xyz, w.xyz, tmin, tmax} + flags
+    // (bit 0 any-hit); cap_count counts them all, cap_max bounds what is written
+    float4* cap_rays;
+    uint32_t* cap_flags;
+    unsigned long long* cap_count;
+    unsigned long long cap_max;
 };
 
 // Launch the kernel for (mode, trav); detail = counting instantiation.
@@ -101,6 +115,12 @@ size_t bvh_deep_bytes(int num_cus, int waves_per_cu);
 // rt_trace_rays: one walk per ray (k_query); bvh_deep sized bvh_deep_bytes(num_cus, 16)
 int launch_query(const DevScene& s, rt_traverse trav, const float* rays, const uint32_t* flags, uint32_t n,
                  rt_ray_hit* out, uint32_t* bvh_deep, int num_cus, hipStream_t stream);
+
+// rt_trace_batch: the traversal-only persistent kernel (k_trace) over n device
+// rays (8 floats each) into n x {record offset | 0xFFFFFFFE any-hit | ~0 miss, dist};
+// work: 1 KiB of shard heads (zeroed here); BSP only
+int launch_trace_batch(const DevScene& s, const float* rays, const uint32_t* flags, uint32_t n, uint32_t* hits,
+                       uint32_t* work, uint32_t threshold, int num_cus, hipStream_t stream);
 
 // Progressive average of one pass's per-iteration samples into accum/ids (after k_path).
 int launch_fold(const DevLaunch& l, hipStream_t stream);
@@ -141,12 +161,14 @@ int build_bsp_device(const float4* pos, const uint4* idx, uint32_t ntris, uint32
 // then the 48-B records; box_scratch: nnodes x 64 B of device memory for the
 // content boxes and the certification data
 constexpr uint32_t BSP_TREELET_BYTES = 96;
-// the camera term H of every treelet for the camera-ray eye (scratch: nnodes floats)
+// the camera terms of every treelet for the camera-ray eye, and each node's
+// silhouette data for RT_BSP_CULL_SILHOUETTE (sil: (nnodes + 1) x 16 B; scratch: nnodes x 24 B)
 int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, const uint4* idx, const uint32_t* ids,
-                      uint32_t nids, const float eye[3], void* blob, void* scratch, hipStream_t stream);
+                      uint32_t nids, const float eye[3], void* blob, uint32_t* sil, void* scratch, hipStream_t stream);
+// tm: nids x {triangle id, material} in treeIds order (or null)
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
                       const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,
-                      void* box_scratch, hipStream_t stream);
+                      void* box_scratch, uint2* tm, hipStream_t stream);
 // device primitives shared by the builders (rt_build.hip)
 int scan_exclusive_u32(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* scratch, hipStream_t s);
 size_t scan_scratch_words(uint32_t n);

@@ -697,16 +697,20 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 #define RT_AB_CULL_CAM 1
 #endif
 __device__ __forceinline__ float h2f(uint32_t bits) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits); }
-// CERT false: the fast margin's formula alone, m = max(|o|inf ko, dscene), for a
-// context whose culling is not RT_BSP_CULL_CERTIFIED (the host picks k_path's
+// CM 0: the fast margin's formula alone, m = max(|o|inf ko, dscene), for a
+// context whose culling is not certified (the host picks k_path's
 // instantiation, so the fast and off modes do not pay for the certified terms;
-// off keeps the +inf gap factor either way).  The generic (CERT true) form
+// off keeps the +inf gap factor either way).  The generic (CM 1) form
 // evaluates every mode from its data constants.
-template <bool CERT = true>
-__device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, const v4u q1, const v4u q5, const f3 o,
-                                             const f3 w, const f3 inv, float tmin, float tmax, float& lo, float& hi)
+// CM: the margin formula -- 0 the fast margin's alone, 1 certified (the generic
+// form every mode's data evaluates), 2 certified with the silhouette bound of
+// camera rays (RT_BSP_CULL_SILHOUETTE, q6 = the node's DevScene.bsp_sil entry)
+template <int CM = 1>
+__device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, const v4u q1, const v4u q5, const v4u q6,
+                                             const f3 o, const f3 w, const f3 inv, float tmin, float tmax, float& lo,
+                                             float& hi)
 {
-    constexpr bool FULL = CERT && RT_AB_CULL_FORMULA != 1;   // (RT_AB_CULL_FORMULA 1: A/B only)
+    constexpr bool FULL = CM >= 1 && RT_AB_CULL_FORMULA != 1;   // (RT_AB_CULL_FORMULA 1: A/B only)
     const float oo[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
     // vectors from the origin to the box's faces; D1 bounds |v0 - o|_1 over the box
     float dl[3], dh[3], D1 = 0.0f;
@@ -742,7 +746,20 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
         const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
         const float winf = __builtin_fmaxf(__builtin_fmaxf(rt_absf(w.x), rt_absf(w.y)), rt_absf(w.z));
         const float dcam = __builtin_fmaf(winf, h2f(q5.x >> 16), 0.0f);   // G: f16 in the high half
-        if (RT_AB_CULL_CAM) den = __builtin_fmaxf(den, cam ? dcam : 0.0f);
+        float dc = dcam;
+        if constexpr (CM == 2) {
+            // RT_BSP_CULL_SILHOUETTE: the subtree's two triangles of smallest camera
+            // term are bounded per ray by their own normals x = n*/E_t^2 (f16, q6; NaN
+            // slots drop out of the minimum), the rest by G_x (q6.w): |denom| / E_t^2
+            // >= min(|w . x| - 2^-9 |w|1, G_x |w|inf) (k_treelet_hcam)
+            const float x0 = __builtin_fmaf(w.z, h2f(q6.y & 0xFFFFu), __builtin_fmaf(w.y, h2f(q6.x >> 16),
+                                                                                     __builtin_fmaf(w.x, h2f(q6.x & 0xFFFFu), 0.0f)));
+            const float x1 = __builtin_fmaf(w.z, h2f(q6.z >> 16), __builtin_fmaf(w.y, h2f(q6.z & 0xFFFFu),
+                                                                                __builtin_fmaf(w.x, h2f(q6.y >> 16), 0.0f)));
+            const float dx = __builtin_fmaf(-0x1p-9f, w1, __builtin_fminf(rt_absf(x0), rt_absf(x1)));
+            dc = __builtin_fmaxf(dcam, __builtin_fminf(dx, __builtin_fmaf(winf, h2f(q6.w & 0xFFFFu), 0.0f)));
+        }
+        if (RT_AB_CULL_CAM) den = __builtin_fmaxf(den, cam ? dc : 0.0f);
         // (fused: fewer roundings than the proof's constants allow for)
         m = __builtin_fmaf(D1, __builtin_fmaf(S.cull_k1 * w1, __builtin_amdgcn_rcpf(den), S.cull_k3), m);
     }
@@ -788,16 +805,16 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
 // trip); an empty leaf, or a subtree culled by its content box, sets pop.
 // (Testing the first record of a leaf in the trip that reaches it -- one more
 // round trip -- was slower: config 4 -3.7 %, config 5 -11 %, profiles/r02/ab_et1.txt.)
-template <bool COUNT, bool CERT = true>
+template <bool COUNT, int CM = 1>
 __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4u q0, const v4u q1, const v4u q2,
-                                         const v4u q3, const v4u q4, const v4u q5, const f3 o, const f3 d, const f3 inv,
-                                         Trav& t, Counters& c, bool& pop)
+                                         const v4u q3, const v4u q4, const v4u q5, const v4u q6, const f3 o, const f3 d,
+                                         const f3 inv, Trav& t, Counters& c, bool& pop)
 {
     uint32_t m = t.node;
     float lo = t.tmin, hi = t.tmax;   // the decisions' interval
     if (RT_BSP_CULL) {
         float blo, bhi;
-        if (bsp_box_miss<CERT>(S, q0, q1, q5, o, d, inv, t.tmin, t.tmax, blo, bhi)) {
+        if (bsp_box_miss<CM>(S, q0, q1, q5, q6, o, d, inv, t.tmin, t.tmax, blo, bhi)) {
             if (COUNT) c.v[C_CULLS]++;
             pop = true;
             return false;
@@ -834,7 +851,7 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
     return leaf & !pop;
 }
 
-template <bool COUNT, bool CULL, class LOG, bool CERT = true>
+template <bool COUNT, bool CULL, class LOG, int CM = 1>
 __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                              bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
@@ -851,9 +868,19 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 48u, 0, 0);
     v4u q4 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 64u, 0, 0);
     v4u q5 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 80u, 0, 0);
+    // (RT_BSP_CULL_SILHOUETTE: a seventh, the node's silhouette data, from its own
+    // array; a leaf lane's is unused)
+    v4u q6 = {0u, 0u, 0u, 0u};
     // keep the loads together (the compiler would sink the later ones
     // into the level-2 branch: a second round trip)
-    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5));
+    if constexpr (CM == 2) {
+        const __amdgpu_buffer_rsrc_t rs6 = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)S.bsp_sil, (short)0, (int)((S.bsp_bytes / BSP_TREELET_BYTES) * 16u), 0x00020000);
+        q6 = __builtin_amdgcn_raw_buffer_load_b128(rs6, t.node * 16u, 0, 0);
+        asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6));
+    } else {
+        asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5));
+    }
     if (COUNT) {   // diagnostics: cycles from issuing the loads to their data
         tw = __builtin_amdgcn_s_memtime() - tw;
         if ((threadIdx.x & 63u) == (uint32_t)__builtin_amdgcn_readfirstlane(threadIdx.x & 63u))
@@ -872,7 +899,7 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     }
 #endif
     if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg);
-    else bsp_walk<COUNT, CERT>(S, stk, q0, q1, q2, q3, q4, q5, o, d, inv, t, c, pop);
+    else bsp_walk<COUNT, CM>(S, stk, q0, q1, q2, q3, q4, q5, q6, o, d, inv, t, c, pop);
 #if RT_AB_EXTRA_LIVE
 #pragma unroll
     for (int i = 0; i < RT_AB_EXTRA_LIVE; i++) asm volatile("" : : "v"(xl[i]));
@@ -880,12 +907,12 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     if (pop) done = bsp_pop(stk, t);
     return done;
 }
-template <bool COUNT, bool CULL = false, bool CERT = true>
+template <bool COUNT, bool CULL = false, int CM = 1>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
 {
     NoLog lg;
-    return bsp_step_log<COUNT, CULL, NoLog, CERT>(S, stk, o, d, inv, anyhit, t, c, lg);
+    return bsp_step_log<COUNT, CULL, NoLog, CM>(S, stk, o, d, inv, anyhit, t, c, lg);
 }
 
 // RN(1/denom) per axis (denom as bsp.wgsl:63): the approximate interior-node
@@ -1144,13 +1171,13 @@ __device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float
     if (TRAV == RT_TRAVERSE_BVH) bvh_init(t, tmin, tmax);
     else trav_init(t, tmin, tmax);
 }
-template <int TRAV, bool COUNT, bool CULL = false, bool CERT = true>
+template <int TRAV, bool COUNT, bool CULL = false, int CM = 1>
 __device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const BvhDeep& dp, const f3 o, const f3 d,
                                           const f3 inv, bool anyhit, Trav& t, Counters& c)
 {
     if (TRAV == RT_TRAVERSE_BVH)
         return bvh_step<COUNT, CULL>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv, anyhit, t, c);
-    return bsp_step<COUNT, CULL, CERT>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
+    return bsp_step<COUNT, CULL, CM>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
 }
 
 // Whole traversal of one ray (used by the primary-ray kernel).
@@ -1186,8 +1213,18 @@ __device__ __forceinline__ HitRec resolve(const DevScene& S, const TraceOut& t, 
     const uint8_t* base = TRAV == RT_TRAVERSE_BVH ? S.bvh_base : reinterpret_cast<const uint8_t*>(S.bsp_nodes);
     const uint32_t slot = (t.k - (TRAV == RT_TRAVERSE_BVH ? S.bvh_rec_off : S.bsp_rec_off)) / 48u;
     const float4* r2p = reinterpret_cast<const float4*>(base + t.k + 32u);
-    h.tri = (TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids)[slot];
-    const uint4 ix = S.tri_idx[h.tri];
+    uint4 ix;
+    if (TRAV == RT_TRAVERSE_BSP) {
+        // {triangle id, material} of the slot in one load (DevScene.bsp_tm); the
+        // vertex indices only where vertex normals are interpolated
+        const uint2 tm = S.bsp_tm[slot];
+        h.tri = tm.x;
+        ix.w = tm.y;
+        if (!face_normals) ix = S.tri_idx[h.tri];
+    } else {
+        h.tri = S.bvh_ids[slot];
+        ix = S.tri_idx[h.tri];
+    }
     h.pos = add(o, muls(d, t.dist));
     f3 n0, n1, n2;
     if (face_normals) {
@@ -1492,10 +1529,30 @@ __device__ __forceinline__ bool w8_ball_shade(const W8Ball& b, f3& ro, f3& rd, f
 // pressure enough to spill inside the traversal loop.
 constexpr int MODE_W9E1_TRANSPARENT = 100 + RT_MODE_W9E1;
 
-// CERT: the BSP walk's margin formula (bsp_box_miss): true, the generic form every
-// culling mode runs correctly with; false, the fast margin's alone (launch_path
-// picks it for W9E1 when the context's culling is not certified)
-template <int MODE, int TRAV, bool COUNT, bool CERT = true>
+// CM: the BSP walk's margin formula (bsp_box_miss): 1, the generic form every
+// culling mode runs correctly with; 0, the fast margin's alone (launch_path picks
+// it for W9E1 / W7E3 when the context's culling is not certified); 2, the certified
+// form with the silhouette bound (RT_BSP_CULL_SILHOUETTE, W9E1)
+// Ray capture of the counting instantiation (DevLaunch.cap_*, rt_set_ray_capture):
+// the ray a walk is about to trace, appended in issue order.  Compiles to
+// nothing in the timed instantiations.
+template <bool COUNT>
+__device__ __forceinline__ void capture_ray(const DevLaunch& L, const f3 o, const f3 d, float tmin, float tmax,
+                                            bool anyhit)
+{
+    if constexpr (COUNT) {
+        if (L.cap_rays) {
+            const unsigned long long i = atomicAdd(L.cap_count, 1ull);
+            if (i < L.cap_max) {
+                L.cap_rays[2 * i] = make_float4(o.x, o.y, o.z, d.x);
+                L.cap_rays[2 * i + 1] = make_float4(d.y, d.z, tmin, tmax);
+                L.cap_flags[i] = anyhit ? 1u : 0u;
+            }
+        }
+    }
+}
+
+template <int MODE, int TRAV, bool COUNT, int CM = 1>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
     TRAV == RT_TRAVERSE_BVH ? RT_BVH_WAVES_PER_EU : MODE == RT_MODE_W7E3 ? RT_W7E3_WAVES_PER_EU : RT_PATH_WAVES_PER_EU,
     8)))
@@ -1582,6 +1639,7 @@ k_path(DevScene S, DevLaunch L)
         shadow = false;
         inv = trav_inv<TRAV>(rd);
         trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
+        capture_ray<COUNT>(L, ro, rd, ETA, ray_tmax<MODE>(ro, rd, ETA), false);
         st = ST_TRACE;
         ao = false;
         hph = 0;
@@ -1638,7 +1696,7 @@ k_path(DevScene S, DevLaunch L)
             }
             const bool go = st == ST_TRACE;
             if (go) {
-                if (trav_step<TRAV, COUNT, W9E3, CERT>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                if (trav_step<TRAV, COUNT, W9E3, CM>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }
             // further steps before the next check: the check (two ballots, a
             // popcount, the compares) is SALU work, and the SALU is a per-CU
@@ -1646,7 +1704,7 @@ k_path(DevScene S, DevLaunch L)
 #pragma unroll
             for (int k = 1; k < (COUNT ? 1 : TRAV == RT_TRAVERSE_BVH ? RT_BVH_TRIPS_PER_CHECK : RT_TRIPS_PER_CHECK); ++k) {
                 if (st == ST_TRACE) {
-                    if (trav_step<TRAV, COUNT, W9E3, CERT>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                    if (trav_step<TRAV, COUNT, W9E3, CM>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
                 }
             }
         }
@@ -1735,6 +1793,7 @@ k_path(DevScene S, DevLaunch L)
                             st = ST_SHADE;
                         } else {
                             trav_start<TRAV>(tr, stk, ETA, Lt.dist - ETA);
+                            capture_ray<COUNT>(L, ro, rd, ETA, Lt.dist - ETA, true);
                         }
                     } else if (sel == 2u || (XT && sel == TSEL)) {
                         f3 n = h.nrm;
@@ -1789,6 +1848,7 @@ k_path(DevScene S, DevLaunch L)
                             bounce++;
                             inv = trav_inv<TRAV>(rd);
                             trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
+                            capture_ray<COUNT>(L, ro, rd, ETA, ray_tmax<MODE>(ro, rd, ETA), false);
                             st = ST_TRACE;
                             cnt.v[C_BOUNCE]++;
                         } else {
@@ -1889,6 +1949,7 @@ k_path(DevScene S, DevLaunch L)
                     else rd = ndir;   // origin = hit position, already in ro
                     inv = trav_inv<TRAV>(rd);
                     trav_start<TRAV>(tr, stk, ETA, ray_tmax<MODE>(ro, rd, ETA));
+                    capture_ray<COUNT>(L, ro, rd, ETA, ray_tmax<MODE>(ro, rd, ETA), false);
                     emit = false;
                     bounce++;
                     shadow = false;
@@ -2209,11 +2270,11 @@ __global__ void __launch_bounds__(256) k_primary(DevScene S, DevLaunch L, int pr
 
 // ------------------------------------------------------------------ ray queries
 // rt_trace_rays: one walk per ray with the render kernels' own step functions
-// (bsp_step / bvh_step): intersect_trimesh (bsp.wgsl:10-81) or intersect_bvh
+// (bsp_step / bvh_step, with the culling mode's margin formula CM): intersect_trimesh (bsp.wgsl:10-81) or intersect_bvh
 // (bvh.wgsl:154-191) for a closest-hit ray, the any-hit walk of the shadow
 // rays (flags bit 0; bsp.wgsl:83-155 stops at the first accept) otherwise.
 // One ray per lane, grid-stride; the tested triangles are hashed in order.
-template <int TRAV>
+template <int TRAV, int CM = 1>
 __global__ void __launch_bounds__(256) k_query(DevScene S, const float* rays, const uint32_t* flags, uint32_t n,
                                                rt_ray_hit* out, uint32_t* bvh_deep)
 {
@@ -2239,8 +2300,8 @@ __global__ void __launch_bounds__(256) k_query(DevScene S, const float* rays, co
             const bool done = TRAV == RT_TRAVERSE_BVH
                                   ? bvh_step_log<false, false>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv,
                                                                anyhit, t, cnt, lg)
-                                  : bsp_step_log<false, false>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t,
-                                                               cnt, lg);
+                                  : bsp_step_log<false, false, FnvLog, CM>(S, reinterpret_cast<float*>(stk), o, d, inv,
+                                                                           anyhit, t, cnt, lg);
             if (done) break;
         }
         rt_ray_hit h;
@@ -2256,6 +2317,88 @@ __global__ void __launch_bounds__(256) k_query(DevScene S, const float* rays, co
         h.tmin = t.tmin;
         h.tmax = t.tmax;
         out[i] = h;
+    }
+}
+
+// ------------------------------------------------------------------ batch trace
+// rt_trace_batch: the trace stage of a wavefront renderer -- device-resident
+// rays in, one hit record per ray out, no shading state.  A persistent grid
+// like k_path's (8 waves per SIMD, the BSP trail in LDS, refills by ballot +
+// mbcnt from 8 per-XCD shards of 64-ray blocks, eight steps per check) whose
+// lanes hold only the walk: o, w, the reciprocals, the interval and the trail
+// state.  Finished lanes wait until at most T lanes of the wave still trace,
+// then refill together (k_path's shading threshold, without the shading).
+// Rays: 32 B {o.xyz, w.xyz, tmin, tmax} (rt_trace_rays' layout), flags bit 0 =
+// any-hit (the shadow walk).  Hits: {record byte offset of the accepted triangle (closest hit) or
+// 0xFFFFFFFE (any-hit: blocked), 0xFFFFFFFF on a miss | dist bits}.
+// DESIGN.md section 4 "Outside the megakernel": the price of a wavefront split.
+template <int CM>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RT_PATH_WAVES_PER_EU, 8)))
+k_trace(DevScene S, const float4* rays, const uint32_t* flags, uint32_t n, uint2* hits, uint32_t* work,
+        uint32_t T)
+{
+    extern __shared__ uint32_t lds_stack[];
+    float* stk = reinterpret_cast<float*>(lds_stack) + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63u;
+    Counters cnt;
+    bool busy = false, anyhit = false, exhausted = n == 0u;
+    uint32_t ri = 0;
+    f3 o = V(0, 0, 0), d = V(0, 0, 1), inv = V(0, 0, 0);
+    Trav tr;
+    trav_init(tr, 0.0f, 0.0f);
+    const uint32_t nblk = (n + 63u) >> 6;   // 64-ray blocks, dealt to the shards round-robin
+    for (;;) {
+        // ---- refill the idle lanes (one atomic per wave and refill)
+        uint32_t shard = shard_of_wave(), tried = 0;
+        for (;;) {
+            const uint64_t need = __ballot(!busy && !exhausted);
+            if (need == 0) break;
+            const uint32_t leader = (uint32_t)__ffsll((unsigned long long)need) - 1u;
+            uint32_t base = 0;
+            if (lane == leader) {
+                const uint32_t head = atomicAdd(work + shard * 32u, (uint32_t)__popcll(need));
+                base = head < (1u << 28) ? head : (1u << 28);
+            }
+            base = __shfl(base, (int)leader, 64);
+            bool ran_out = false;
+            if (!busy && !exhausted) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0u));
+                const uint32_t h = base + rank;
+                const uint32_t blk = ((h >> 6) << RT_SHARD_LG) + shard;
+                const uint32_t i = (blk << 6) | (h & 63u);
+                if (blk >= nblk) {
+                    ran_out = true;
+                } else if (i < n) {
+                    const float4 a = rays[2 * (size_t)i], b = rays[2 * (size_t)i + 1];   // o.xyz w.x | w.yz tmin tmax
+                    o = V(a.x, a.y, a.z);
+                    d = V(a.w, b.x, b.y);
+                    anyhit = flags && (flags[i] & 1u);
+                    inv = bsp_inv(d);
+                    trav_start<RT_TRAVERSE_BSP>(tr, stk, b.z, b.w);
+                    ri = i;
+                    busy = true;
+                }
+            }
+            if (__ballot(ran_out) != 0) {   // this shard is drained (its head only grows)
+                shard = (shard + 1u) & ((1u << RT_SHARD_LG) - 1u);
+                if (++tried == (1u << RT_SHARD_LG)) exhausted = true;
+            }
+        }
+        if (__ballot(busy) == 0) break;
+        // ---- trace until at most T lanes are busy (every lane, once the rays ran out)
+        for (;;) {
+            const uint64_t bm = __ballot(busy);
+            if (bm == 0 || (!exhausted && (uint32_t)__popcll(bm) <= T)) break;
+#pragma unroll
+            for (int k = 0; k < RT_TRIPS_PER_CHECK; ++k) {
+                if (busy && bsp_step<false, false, CM>(S, stk, o, d, inv, anyhit, tr, cnt)) {
+                    busy = false;
+                    const uint32_t hk = !tr.found ? 0xFFFFFFFFu : anyhit ? 0xFFFFFFFEu : tr.hit_k;
+                    hits[ri] = make_uint2(hk, __float_as_uint(tr.tmax));
+                }
+            }
+        }
     }
 }
 
@@ -2732,7 +2875,13 @@ static void launch_path(const DevScene& s, const DevLaunch& l, int grid, size_t 
     // certified terms (round 3's trip).  The other modes run the generic formula.
     if constexpr ((MODE == RT_MODE_W9E1 || MODE == RT_MODE_W7E3) && TRAV == RT_TRAVERSE_BSP) {
         if (s.cull_k1 == 0.0f) {
-            hipLaunchKernelGGL((k_path<MODE, TRAV, COUNT, false>), dim3(grid), dim3(256), lds, st, s, l);
+            hipLaunchKernelGGL((k_path<MODE, TRAV, COUNT, 0>), dim3(grid), dim3(256), lds, st, s, l);
+            return;
+        }
+    }
+    if constexpr (MODE == RT_MODE_W9E1 && TRAV == RT_TRAVERSE_BSP) {
+        if (s.bsp_cull_mode == RT_BSP_CULL_SILHOUETTE) {
+            hipLaunchKernelGGL((k_path<MODE, TRAV, COUNT, 2>), dim3(grid), dim3(256), lds, st, s, l);
             return;
         }
     }
@@ -2869,9 +3018,33 @@ int launch_query(const DevScene& s, rt_traverse trav, const float* rays, const u
     if (trav == RT_TRAVERSE_BVH)
         hipLaunchKernelGGL(k_query<RT_TRAVERSE_BVH>, dim3(blocks), dim3(256), lds, stream, s, rays, flags, n, out,
                            bvh_deep);
-    else
-        hipLaunchKernelGGL(k_query<RT_TRAVERSE_BSP>, dim3(blocks), dim3(256), lds, stream, s, rays, flags, n, out,
+    else if (s.cull_k1 == 0.0f)   // the culling mode's formula, as the render kernels pick it (launch_path)
+        hipLaunchKernelGGL((k_query<RT_TRAVERSE_BSP, 0>), dim3(blocks), dim3(256), lds, stream, s, rays, flags, n, out,
                            bvh_deep);
+    else if (s.bsp_cull_mode == RT_BSP_CULL_SILHOUETTE)
+        hipLaunchKernelGGL((k_query<RT_TRAVERSE_BSP, 2>), dim3(blocks), dim3(256), lds, stream, s, rays, flags, n, out,
+                           bvh_deep);
+    else
+        hipLaunchKernelGGL((k_query<RT_TRAVERSE_BSP, 1>), dim3(blocks), dim3(256), lds, stream, s, rays, flags, n, out,
+                           bvh_deep);
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+
+int launch_trace_batch(const DevScene& s, const float* rays, const uint32_t* flags, uint32_t n, uint32_t* hits,
+                       uint32_t* work, uint32_t threshold, int num_cus, hipStream_t stream)
+{
+    const size_t lds = (size_t)(s.bsp_depth ? s.bsp_depth : 1) * 256 * 4;
+    const int lds_waves = 4 * (int)((160u * 1024u) / lds);
+    const int grid = grid_for(num_cus, std::min(4 * RT_PATH_WAVES_PER_EU, std::max(4, lds_waves)));
+    if (hipMemsetAsync(work, 0, 8 * 128, stream) != hipSuccess) return RT_E_DEVICE;
+    const float4* r = reinterpret_cast<const float4*>(rays);
+    uint2* h = reinterpret_cast<uint2*>(hits);
+    if (s.cull_k1 == 0.0f)
+        hipLaunchKernelGGL(k_trace<0>, dim3(grid), dim3(256), lds, stream, s, r, flags, n, h, work, threshold);
+    else if (s.bsp_cull_mode == RT_BSP_CULL_SILHOUETTE)
+        hipLaunchKernelGGL(k_trace<2>, dim3(grid), dim3(256), lds, stream, s, r, flags, n, h, work, threshold);
+    else
+        hipLaunchKernelGGL(k_trace<1>, dim3(grid), dim3(256), lds, stream, s, r, flags, n, h, work, threshold);
     return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }
 

@@ -98,7 +98,7 @@ def cpu_baseline(wl, trav, mesh, accel, spp, W, H, budget_s):
 
 def pmc_key(W, H, spp, trav, world, config, cull=1):
     return (f"{W}x{H}x{spp}_{trav}_n{world}" + ("" if config == 3 else f"_c{config}") +
-            {0: "_off", 1: "", 2: "_fast"}[cull if trav == "BSP" else 1])
+            {0: "_off", 1: "", 2: "_fast", 3: "_sil"}[cull if trav == "BSP" else 1])
 
 
 def fatbin_sha16(path):
@@ -214,7 +214,8 @@ def main():
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)
     ap.add_argument("--bsp-cull", type=int, default=None,
-                    help="RT_OPT_BSP_CULL: 0 off, 1 certified (the library default), 2 fast margin")
+                    help="RT_OPT_BSP_CULL: 0 off, 1 certified (the library default), 2 fast margin, "
+                         "3 certified + silhouette bound")
     ap.add_argument("--async-fold", action="store_true",
                     help="pipelined frames (RT_OPT_ASYNC_FOLD 1): a frame's fold and gather overlap the next "
                          "frame's traversal kernel (measured slower on config 3: profiles/r04/ab_async_fold.txt)")
@@ -419,7 +420,7 @@ def main():
         # rank 0's share (profiles/pmc_summary.json key _n<N>, measured with --rank-share N)
         bytes_per_launch = rays[4] / (world if use_dist else 1) / max(1, launches_per_step)
         cull = args.bsp_cull if args.bsp_cull is not None else rt._ffi.RT_BSP_CULL_CERTIFIED
-        cull_name = {0: "off", 1: "certified", 2: "fast"}[cull] if trav == "BSP" else None
+        cull_name = {0: "off", 1: "certified", 2: "fast", 3: "silhouette"}[cull] if trav == "BSP" else None
         roof = roofline(pmc_key(W, H, spp, trav, nsplit, args.config, cull), kern_ms_own, bytes_per_launch, args.config,
                         f"k_path<{wl.mode},{trav}>")
         roof["launches_per_step"] = launches_per_step

@@ -199,6 +199,12 @@ typedef struct rt_ray_counts {
                                      f32 test's hit point can sit off the triangle by more than the margin, can get
                                      a different hit (measured: 2 of 400,000 deliberately grazing rays on a random
                                      soup, none in any rendered frame) */
+#define RT_BSP_CULL_SILHOUETTE 3  /* the certified margin, exact as RT_BSP_CULL_CERTIFIED, with a tighter bound for
+                                     camera rays: each subtree's two triangles nearest the eye's plane-distance
+                                     floor (its silhouette) are bounded per ray by their own normals, the rest by
+                                     their camera term.  Fewer trips for far, many-object views (config 4: +15 %),
+                                     more arithmetic per trip (config 3: -4 %, config 5: -6 %): opt-in.  The W9E1
+                                     path kernel and rt_trace_batch use it; other kernels run the certified form */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
 
@@ -335,9 +341,12 @@ int rt_download_bsp(rt_ctx* ctx, uint32_t* tree, float* planes, uint32_t cap_nod
  * BSP walk's 96-B treelets (slot 0 unused, then one per 1-based node M:
  * content box, nodes M, 2M, 2M+1, 4M..4M+3, and the certified culling's data
  * -- F bf16 | camera term G f16 << 16, normal-box centre and radius as f16;
- * rt_bsp_build.hip k_bsp_repack) to dst, (nnodes + 1) * 96 bytes, after
- * bringing the camera terms up to date for the uniforms' eye (certified
- * culling).  The size is stored in *bytes (pass dst NULL to query it). */
+ * rt_bsp_build.hip k_bsp_repack) to dst, (nnodes + 1) * 96 bytes, followed by
+ * RT_BSP_CULL_SILHOUETTE's node data ((nnodes + 1) * 16 bytes: the two excluded
+ * triangles' n* / E^2 as f16 triples, the rest's camera term G_x f16; zero when
+ * not computed), after bringing the camera terms up to date for the uniforms'
+ * eye (certified culling).  The size is stored in *bytes (pass dst NULL to
+ * query it). */
 int rt_download_bsp_treelets(rt_ctx* ctx, void* dst, uint64_t cap_bytes, uint64_t* bytes);
 
 /* Copy the context's BVH in the reference layout (GpuNode array, bvh_triangles)
@@ -439,6 +448,29 @@ int rt_comm_destroy(rt_ctx* ctx);
  * stream has drained.  Either id pointer may be NULL on every rank (accum only). */
 int rt_gather_tiles(rt_ctx* ctx, uint32_t width, uint32_t height, const float* local_accum,
                     const uint32_t* local_ids, float* frame_accum, uint32_t* frame_ids);
+
+/* ---- the trace stage of a wavefront renderer ---------------------------------
+ * rt_trace_batch walks n device-resident rays through the context's BSP with the
+ * render kernels' step function in a traversal-only persistent kernel (no
+ * shading state; refills by ballot + mbcnt from per-XCD queues): rays_dev = n x
+ * {o.xyz, w.xyz, tmin, tmax} (f32, rt_trace_rays' layout), flags_dev = n x u32 (bit 0: any-hit, the
+ * shadow walk; NULL: every ray closest-hit), hits_dev = n x {u32 record byte
+ * offset of the accepted triangle (closest hit), 0xFFFFFFFE (any-hit: blocked) or
+ * 0xFFFFFFFF (miss), f32 dist}.  The results are rt_trace_rays' walks (same
+ * culling mode).  Asynchronous on the context stream; timed by
+ * RT_OPT_KERNEL_TIMING like the render kernels.  RT_OPT_SHADE_THRESHOLD's low
+ * byte (default 16) is the lanes-still-tracing count at which finished lanes
+ * refill.  DESIGN.md section 4 "Outside the megakernel".
+ *
+ * rt_set_ray_capture arms a capture: every counting render (RT_OPT_DETAIL_COUNTERS)
+ * of a W7E3 / W9E1 path mode appends each ray its walks start -- camera, shadow
+ * and bounce rays, in issue order -- to rays_dev / flags_dev in the layout above
+ * (up to cap rays; NULL disarms); rt_ray_capture_count returns how many were
+ * traced since it was armed (more than cap: the rest were not written). */
+int rt_trace_batch(rt_ctx* ctx, rt_traverse trav, const float* rays_dev, const uint32_t* flags_dev, uint32_t n,
+                   uint32_t* hits_dev);
+int rt_set_ray_capture(rt_ctx* ctx, float* rays_dev, uint32_t* flags_dev, uint64_t cap);
+int rt_ray_capture_count(rt_ctx* ctx, uint64_t* n);
 
 /* ---- ray queries: the walk alone ------------------------------------------ */
 

@@ -11,7 +11,13 @@ the reference-layout tree (rt_download_bsp):
     e0 x e1 exactly and E2s = E2 rounded up to f32 (the repack's divisor);
   * the camera term G (f16) <= (H - 128u D1) / Dinf for the uniforms' eye, H the
     subtree's least |(v0 - eye) . n*| / E_T^2 and D1, Dinf the L1 / L-inf
-    distances of the stored box from the eye.
+    distances of the stored box from the eye;
+  * (round 5, RT_BSP_CULL_SILHOUETTE's node data) the two triangles of least H
+    are stored as their normals n*/E_t^2 (f16, nearest) and the rest's term
+    G_x <= (H3 - 128u D1) / Dinf, H3 the
+    third least H of distinct triangles -- recomputed here with the GPU's own
+    order (stable in H, leaves in treeIds order, a subtree's left child first),
+    so the stored normals must be exactly those triangles'.
 
 Rounding the wrong way anywhere in those kernels would break the proof without
 necessarily changing a test frame; this pins each inequality."""
@@ -44,12 +50,12 @@ def _check(rt, mesh, eye, target):
         ctx.upload_mesh(mesh)
         ctx.upload_bsp(mesh.bsp_tree())
         ctx.set_uniforms(rt.make_uniform(tuple(float(x) for x in eye), target, (0.0, 1.0, 0.0), 1.5, 64, 64))
-        tl = ctx.download_bsp_treelets()
+        tl, sil = ctx.download_bsp_treelets(silhouette=True)
         tree, planes, ids, aabb = ctx.download_bsp()
     finally:
         ctx.close()
     n = tree.shape[0]
-    assert tl.shape == (n + 1, 24)
+    assert tl.shape == (n + 1, 24) and sil.shape == (n + 1, 4)
 
     # per triangle, from the records' f32 edges (k_tri_records2)
     P = V[:, :3].astype(np.float32)
@@ -138,10 +144,80 @@ def _check(rt, mesh, eye, target):
     Gt = np.maximum(Gt, 0.0)
     assert (G[fin] <= Gt[fin]).all(), "camera term above its bound"
     assert (G[fin] >= 0).all()
+    # the excluded pair and G_x (k_leaf_hcam / k_node_hcam / k_treelet_hcam), in the
+    # GPU's own f32 values of H (tri_hcam: |dot| less its error bound, rounded down)
+    dot = d[:, 0] * ns[:, 0] + d[:, 1] * ns[:, 1] + d[:, 2] * ns[:, 2]
+    err = 2.0 ** -45 * (np.abs(d[:, 0] * ns[:, 0]) + np.abs(d[:, 1] * ns[:, 1]) + np.abs(d[:, 2] * ns[:, 2]))
+    with np.errstate(divide="ignore", invalid="ignore"):
+        hx = np.where(np.abs(dot) - err > 0, (np.abs(dot) - err) / E2 * (1.0 - 2.0 ** -19), 0.0)
+    hg = hx.astype(np.float32)
+    up_ = hg.astype(np.float64) > hx
+    hg[up_] = np.nextafter(hg[up_], np.float32(-np.inf))
+    Hg = np.where(E2 > 0, hg.astype(np.float64), np.inf)
+    h3, t3 = _top3(tree, ids, Hg, leaf, n)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        Gx_t = np.where(np.isinf(h3[idx, 2]), np.inf,
+                        np.maximum(np.where(Dinf > 0, (h3[idx, 2] - 128 * U * D1) / Dinf, 0.0), 0.0))
+        nt = np.where(E2[:, None] > 0, ns / E2[:, None], np.nan).astype(np.float32).astype(np.float16).view(np.uint16)
+    srow = sil[idx + 1]
+    Gx = _f16((srow[:, 3] & 0xFFFF).astype(np.uint16))
+    assert (Gx <= Gx_t).all(), "excluded camera term above its bound"
+    xs = np.stack([srow[:, 0] & 0xFFFF, srow[:, 0] >> 16, srow[:, 1] & 0xFFFF,
+                   srow[:, 1] >> 16, srow[:, 2] & 0xFFFF, srow[:, 2] >> 16], 1).astype(np.uint16)
+    for j in range(2):
+        tj = t3[idx, j]
+        ok = tj >= 0
+        assert np.array_equal(xs[ok, 3 * j:3 * j + 3], nt[tj[ok]]), f"excluded normal {j}"
+        assert (xs[~ok, 3 * j:3 * j + 3] == 0x7E00).all()
     bound = int((G[fin] > 0).sum())
     print(f"{len(idx)} reachable treelets ({int(has.sum())} with triangles): content boxes, floors, normal boxes "
           f"and {bound} positive camera terms within their bounds")
     return bound
+
+
+def _top3(tree, ids, H, leaf, n):
+    """Per node the three least H of distinct triangles of its subtree and the
+    triangles (-1: none), as k_leaf_hcam / k_node_hcam build them: stable in H
+    over the leaf's treeIds order / the left child's list then the right's, a
+    repeated triangle kept once, +inf never taken."""
+    h3 = np.full((n, 3), np.inf)
+    t3 = np.full((n, 3), -1, np.int64)
+
+    def take(hc, tc):
+        # rows of candidates in insertion order -> the first three of a stable sort
+        o = np.argsort(hc, axis=1, kind="stable")
+        hs = np.take_along_axis(hc, o, 1)
+        ts = np.take_along_axis(tc, o, 1)
+        for j in range(1, ts.shape[1]):   # a triangle seen earlier in the row (same H) is dropped
+            dup = (ts[:, j:j + 1] == ts[:, :j]).any(1) & (ts[:, j] >= 0)
+            hs[dup, j] = np.inf
+            ts[dup, j] = -1
+        o = np.argsort(hs, axis=1, kind="stable")
+        hs = np.take_along_axis(hs, o, 1)[:, :3]
+        ts = np.take_along_axis(ts, o, 1)[:, :3]
+        ts[~np.isfinite(hs)] = -1
+        return hs, ts
+
+    cnt = (tree[:, 0] >> 2).astype(np.int64)
+    first = tree[:, 1].astype(np.int64)
+    lvs = np.nonzero(leaf & (cnt > 0))[0]
+    w = int(cnt[lvs].max()) if len(lvs) else 1
+    hc = np.full((len(lvs), w), np.inf)
+    tc = np.full((len(lvs), w), -1, np.int64)
+    for k in range(w):
+        has = cnt[lvs] > k
+        t = ids[(first[lvs] + k)[has]].astype(np.int64)
+        hc[has, k] = H[t]
+        tc[has, k] = t
+    h3[lvs], t3[lvs] = take(hc, tc)
+    dmax = int(np.floor(np.log2(n + 1)))
+    for dd in range(dmax, -1, -1):
+        i = np.arange(2 ** dd - 1, min(2 ** (dd + 1) - 1, n))
+        i = i[(~leaf[i]) & (2 * i + 2 < n)]
+        if len(i):
+            h3[i], t3[i] = take(np.concatenate([h3[2 * i + 1], h3[2 * i + 2]], 1),
+                                np.concatenate([t3[2 * i + 1], t3[2 * i + 2]], 1))
+    return h3, t3
 
 
 def test_teapot_treelets(rt):

@@ -19,7 +19,7 @@ from parity_util import BUNNY_CAM, CORNELL_CAM, TEAPOT_CAM, Scene
 pytestmark = pytest.mark.gpu
 
 
-CULL_MODES = (0, 1, 2)   # RT_BSP_CULL_OFF, _CERTIFIED (default), _FAST
+CULL_MODES = (0, 1, 2, 3)   # RT_BSP_CULL_OFF, _CERTIFIED (default), _FAST, _SILHOUETTE
 
 
 def _frames(rt, s, mode, cam, W, H, region, spp, selection1=0, jitter=None):
@@ -30,7 +30,7 @@ def _frames(rt, s, mode, cam, W, H, region, spp, selection1=0, jitter=None):
         out.append(s.render_gpu(mode, cam, W, H, region, 0, spp, selection1=selection1, jitter=jitter))
     s.ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, rt._ffi.RT_BSP_CULL_CERTIFIED)
     s.ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
-    for f, name in zip(out[1:], ("certified", "fast")):
+    for f, name in zip(out[1:], ("certified", "fast", "silhouette")):
         print(f"{mode}: {name} culls {f[2]['subtree_culls']}, interior nodes "
               f"{f[2]['node_interior'] / max(1, out[0][2]['node_interior']):.3f} of the unculled walk")
     return out
@@ -47,25 +47,23 @@ def _same(a, b, culled=True):
 
 
 def _all_same(frames, culled=True):
-    off, cert, fast = frames
-    _same(off, cert, culled)
-    _same(off, fast, culled)
+    off, *ons = frames   # certified, fast, silhouette
+    for on in ons:
+        _same(off, on, culled)
 
 
 def test_cornell_w7e3_full_frame(rt):
     # the whole config-2 frame (1024 x 1024) at 8 spp: flat, coplanar walls and
     # the area-light shadow rays that graze the ceiling the light sits in
     s = Scene(rt, rt.Mesh.from_obj(model("CornellBoxWithBlocks.obj")), "BSP")
-    off, on, fast = _frames(rt, s, "W7E3", CORNELL_CAM, 1024, 1024, (0, 0, 1024, 1024), 8)
-    _all_same((off, on, fast))
+    _all_same(_frames(rt, s, "W7E3", CORNELL_CAM, 1024, 1024, (0, 0, 1024, 1024), 8))
     assert on[2]["tri_tests"] <= off[2]["tri_tests"]
     s.ctx.close()
 
 
 def test_bunny_w9e1_frame(rt):
     s = Scene(rt, rt.Mesh.synth_bunny(), "BSP", env=(0.8, 0.9, 1.0))
-    off, on, fast = _frames(rt, s, "W9E1", BUNNY_CAM, 1920, 1080, (0, 0, 1920, 1080), 2)
-    _all_same((off, on, fast))
+    _all_same(_frames(rt, s, "W9E1", BUNNY_CAM, 1920, 1080, (0, 0, 1920, 1080), 2))
     # the point of it: far fewer nodes and triangles
     assert on[2]["node_interior"] < 0.75 * off[2]["node_interior"]
     assert fast[2]["node_interior"] < 0.6 * off[2]["node_interior"]

@@ -10,7 +10,8 @@ random distance (0.01 .. 1), so it grazes that triangle and crosses the cells
 around it; 30 % are any-hit walks (shadow rays).  Scenes: the config-5 style
 random soup (1M large, randomly oriented triangles) and the bunny stand-in.
 
-  * the default walk (RT_BSP_CULL_CERTIFIED) equals the CPU oracle's walk
+  * the default walk (RT_BSP_CULL_CERTIFIED), and the opt-in silhouette bound
+    (RT_BSP_CULL_SILHOUETTE, round 5), equal the CPU oracle's walk
     (bsp.wgsl:10-81, every node visited) ray for ray: triangle and distance
     bit for bit, hit or miss for the any-hit rays -- 0 differences -- and the
     unculled GPU walk in every field (triangle, distance, barycentrics);
@@ -63,7 +64,7 @@ def test_grazing_rays_default_walk_equals_oracle(rt, gpu, oracle, scene):
         ctx.upload_mesh(mesh)
         ctx.upload_bsp(bsp)
         h = {}
-        for name in ("OFF", "FAST", "CERTIFIED"):   # CERTIFIED last: the context's default again
+        for name in ("OFF", "FAST", "SILHOUETTE", "CERTIFIED"):   # CERTIFIED last: the context's default again
             ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, getattr(rt._ffi, "RT_BSP_CULL_" + name))
             h[name] = ctx.trace_rays("BSP", R, anyhit)
     finally:
@@ -86,6 +87,9 @@ def test_grazing_rays_default_walk_equals_oracle(rt, gpu, oracle, scene):
     assert bad.sum() == 0, f"{int(bad.sum())} of {len(R)} grazing rays differ from the oracle's walk"
     for k in ("tri", "dist", "beta", "gamma"):
         assert np.array_equal(h["OFF"][k].view(np.uint32), cert[k].view(np.uint32)), k
+        # RT_BSP_CULL_SILHOUETTE: exact as well (its camera bound does not apply:
+        # these rays do not start at an eye)
+        assert np.array_equal(h["OFF"][k].view(np.uint32), h["SILHOUETTE"][k].view(np.uint32)), k
 
     # the fast margin: measured; each difference is an off-triangle f32 accept
     fast = h["FAST"]
@@ -148,10 +152,13 @@ def test_camera_rays_default_walk_equals_oracle(rt, gpu, oracle, scene):
         ctx.upload_bsp(bsp)
         ctx.set_uniforms(rt.make_uniform(tuple(float(x) for x in eye), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 1.5, 64, 64))
         h_ = {}
-        for name in ("OFF", "FAST", "CERTIFIED"):
+        for name in ("OFF", "FAST", "SILHOUETTE", "CERTIFIED"):
             ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, getattr(rt._ffi, "RT_BSP_CULL_" + name))
             ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
             h_[name] = ctx.trace_rays("BSP", R, anyhit)
+            if name == "SILHOUETTE":   # the mode's node data, for this eye
+                _, sil = ctx.download_bsp_treelets(silhouette=True)
+                assert (sil[1:, 3] != 0).any()
     finally:
         ctx.close()
     MISS = 0xFFFFFFFF
@@ -168,7 +175,11 @@ def test_camera_rays_default_walk_equals_oracle(rt, gpu, oracle, scene):
         badf |= h_["OFF"][k].view(np.uint32) != h_["FAST"][k].view(np.uint32)
     print(f"{scene}: {len(R)} camera rays ({hits} hits): certified vs oracle {int(bad.sum())} differ, "
           f"fast vs unculled {int(badf.sum())} differ")
+    sil_ = h_["SILHOUETTE"]
+    bads = (sil_["tri"] != otri) | ((otri != MISS) & (sil_["dist"].view(np.uint32) != odist.view(np.uint32)))
+    print(f"{scene}: silhouette-bound walk vs oracle {int(bads.sum())} differ")
     assert hits > len(R) // 4
-    assert bad.sum() == 0
+    assert bad.sum() == 0 and bads.sum() == 0
     for k in ("tri", "dist", "beta", "gamma"):
         assert np.array_equal(h_["OFF"][k].view(np.uint32), cert[k].view(np.uint32)), k
+        assert np.array_equal(h_["OFF"][k].view(np.uint32), sil_[k].view(np.uint32)), k

@@ -19,11 +19,12 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 BUDGET = {
     # W9E1, BSP: the bench kernel, eight traversal steps per trip
     # (RT_TRIPS_PER_CHECK); none of them spills
-    "k_pathILi4ELi0ELb0ELb1": 0,
-    "k_pathILi4ELi0ELb0ELb0": 0,   # W9E1, BSP, the fast-margin instantiation
-    "k_pathILi4ELi1ELb0ELb1": 0,   # W9E1, BVH at 8 waves/SIMD (4 before the round-2 spill cuts)
-    "k_pathILi3ELi0ELb0ELb1": 0,
-    "k_pathILi3ELi0ELb0ELb0": 0,   # W7E3, BSP, the fast-margin instantiation   # W7E3, BSP at 7 waves/SIMD
+    "k_pathILi4ELi0ELb0ELi1": 0,
+    "k_pathILi4ELi0ELb0ELi0": 0,   # W9E1, BSP, the fast-margin instantiation
+    "k_pathILi4ELi0ELb0ELi2": 0,   # W9E1, BSP, the silhouette bound
+    "k_pathILi4ELi1ELb0ELi1": 0,   # W9E1, BVH at 8 waves/SIMD (4 before the round-2 spill cuts)
+    "k_pathILi3ELi0ELb0ELi1": 0,
+    "k_pathILi3ELi0ELb0ELi0": 0,   # W7E3, BSP, the fast-margin instantiation   # W7E3, BSP at 7 waves/SIMD
 }
 
 
@@ -56,12 +57,14 @@ WHOLE_BUDGET = {
     # the camera bound (eye compare, |w|inf, the eye term) 108/93 and 68/58; its
     # per-treelet precomputed form 108/93 and 64/56.
     # round 5: the zero-component slab of the cull (an infinite reciprocal, the
-    # capped gap tolerance) and bsp_inv1's flag: 108/99, and W7E3 72/62 / 64/56.
-    "k_pathILi4ELi0ELb0ELb1": (108, 99),    # W9E1, BSP
-    "k_pathILi4ELi0ELb0ELb0": (88, 99),     # W9E1, BSP, the fast-margin instantiation
-    "k_pathILi4ELi1ELb0ELb1": (80, 77),     # W9E1, BVH
-    "k_pathILi3ELi0ELb0ELb1": (72, 62),     # W7E3, BSP at 7 waves/SIMD
-    "k_pathILi3ELi0ELb0ELb0": (64, 56),     # W7E3, BSP, the fast-margin instantiation (0/0 at 5)
+    # capped gap tolerance) and bsp_inv1's flag: 108/99 (W7E3 64/56 and 64/53 with
+    # the one-load hit resolve); the opt-in silhouette bound's instantiation 128/118.
+    "k_pathILi4ELi0ELb0ELi1": (108, 99),    # W9E1, BSP
+    "k_pathILi4ELi0ELb0ELi2": (128, 118),   # W9E1, BSP, RT_BSP_CULL_SILHOUETTE (opt-in)
+    "k_pathILi4ELi0ELb0ELi0": (88, 99),     # W9E1, BSP, the fast-margin instantiation
+    "k_pathILi4ELi1ELb0ELi1": (80, 77),     # W9E1, BVH
+    "k_pathILi3ELi0ELb0ELi1": (64, 56),     # W7E3, BSP at 7 waves/SIMD
+    "k_pathILi3ELi0ELb0ELi0": (64, 53),     # W7E3, BSP, the fast-margin instantiation (0/0 at 5)
 }
 
 

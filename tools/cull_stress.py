@@ -1,8 +1,8 @@
 """Subtree culling at the BASELINE spp of the 8-GPU workloads (DESIGN.md section 4
 "Subtree culling"): the whole config-4 frame at 256 spp and the whole config-5
 frame at 1024 spp (and config 3's at 256), rendered with RT_OPT_BSP_CULL 1
-(certified margin, the default), 2 (fast margin) and 0 (every node of bsp.wgsl's
-walk), compared bit for bit: every pixel's accumulation, the primary-hit ids and
+(certified margin, the default), 3 (certified with the silhouette bound), 2 (fast
+margin) and 0 (every node of bsp.wgsl's walk), compared bit for bit: every pixel's accumulation, the primary-hit ids and
 the ray counts.  Too long for the GPU
 suite (the unculled config-5 frame takes about a minute); run once per kernel
 change, its output committed under profiles/.
@@ -51,13 +51,13 @@ def main():
             ctx.set_environment(wl.env)
             ctx.set_uniforms(rt.make_uniform(*wl.camera, wl.width, wl.height))
             frames = {}
-            for cull, name in ((1, "certified"), (2, "fast"), (0, "unculled")):
+            for cull, name in ((1, "certified"), (3, "silhouette"), (2, "fast"), (0, "unculled")):
                 frames[name] = frame(rt, ctx, wl, cull)
                 print(f"config {n}: {name} frame {frames[name][3]:.1f} s", flush=True)
         finally:
             ctx.close()
         off = frames["unculled"]
-        for name in ("certified", "fast"):
+        for name in ("certified", "silhouette", "fast"):
             on = frames[name]
             px = int((on[0] != off[0]).any(axis=2).sum())
             idm = int((on[1] != off[1]).sum())

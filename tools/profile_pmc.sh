@@ -2,6 +2,7 @@
 # PMC passes over a short bench run (one counter group per rocprofv3 run, as
 # MI355X_MICROARCH.md "rocprofv3 PMC slots" requires).  Writes gpurun_out/prof/<tag>/pmc<i>/.
 # usage: tools/profile_pmc.sh <tag> [bench args...]
+# (PMC_PROG: the python program and its fixed arguments, default "bench.py --no-cpu-baseline")
 set -u
 TAG=$1; shift
 export TMPDIR=/tmp
@@ -16,7 +17,7 @@ PASSES=(
 )
 i=0
 for P in "${PASSES[@]}"; do
-  timeout -k 10 240 rocprofv3 --pmc $P -d $OUT/pmc$i -o pmc --output-format csv -- python bench.py --no-cpu-baseline "$@" > $OUT/pmc$i.log 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $P -d $OUT/pmc$i -o pmc --output-format csv -- python ${PMC_PROG:-bench.py --no-cpu-baseline} "$@" > $OUT/pmc$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc"
   if [ $rc -ne 0 ]; then exit $rc; fi

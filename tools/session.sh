@@ -4,8 +4,12 @@
 # is reported and the session goes on).
 # usage: tools/session.sh <tag> <step...>
 #   tests [pytest args]   the GPU suite (or the named test files: tests:file1,file2)
-#   ab<C>:<v1>,<v2>,..    A/B of variants/<v>/lib02562rt.so on config C (3, 4; 5 at 128 spp)
+#   ab<C>[f]:<v1>,<v2>,.. A/B of variants/<v>/lib02562rt.so on config C (2, 3, 4; 5 at 128 spp;
+#                         f: the fast margin)
 #   m<C>[fast]            bench line + kernel-trace stats + PMC passes (tools/measure.sh)
+#   wf<C>[f] / wfpmc<C>   the wavefront split's price (tools/wavefront_price.py) / its PMC passes
+#   stress                tools/cull_stress.py: configs 3-5 whole frames, every culling mode
+#   sweep<C>[f]:T1,..     shading-threshold sweep (tools/sweep_threshold.sh)
 set -u
 TAG=$1; shift
 export TMPDIR=/tmp
@@ -18,10 +22,33 @@ for step in "$@"; do
       rc=$?; tail -3 $OUT/pytest_gpu.log; grep -E "FAILED|ERROR" $OUT/pytest_gpu.log | head -20
       if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi ;;
     ab*)
-      c=${step:2:1}; vs=$(echo ${step#*:} | tr , ' ')
+      # ab<C>[f|s]:v1,v2,...  (f: the fast margin, --bsp-cull 2; s: the silhouette bound, --bsp-cull 3)
+      c=${step:2:1}; vs=$(echo ${step#*:} | tr , ' '); f=""; fo=""
+      [ "${step:3:1}" = "f" ] && { f=f; fo="--bsp-cull 2"; }
+      [ "${step:3:1}" = "s" ] && { f=s; fo="--bsp-cull 3"; }
       case $c in 3) o="";; 4) o="--config 4";; 5) o="--config 5 --spp 128";; 2) o="--config 2";; esac
-      bash tools/ab.sh $OUT/ab_c$c.txt "$o ${AB_OPTS:-}" $vs || { tail -5 $OUT/ab_c$c.txt; exit 1; }
-      cat $OUT/ab_c$c.txt ;;
+      bash tools/ab.sh $OUT/ab_c$c$f.txt "$o $fo ${AB_OPTS:-}" $vs || { tail -5 $OUT/ab_c$c$f.txt; exit 1; }
+      cat $OUT/ab_c$c$f.txt ;;
+    wf3|wf5|wf3f|wf5f)
+      # the wavefront split's price on the captured ray stream (tools/wavefront_price.py)
+      c=${step:2:1}; fo=""; [ "${step:3:1}" = "f" ] && fo="--bsp-cull 2"
+      timeout -k 10 600 python tools/wavefront_price.py --config $c $fo > $OUT/wf_c$c${step:3:1}.json 2> $OUT/wf_c$c${step:3:1}.err \
+        || { echo "wavefront_price rc=$?"; tail -20 $OUT/wf_c$c${step:3:1}.err; exit 1; }
+      cat $OUT/wf_c$c${step:3:1}.json ;;
+    wfpmc3|wfpmc5)
+      c=${step:5:1}
+      PMC_PROG="tools/wavefront_price.py --reps 1" bash tools/profile_pmc.sh $TAG/wf_c$c --config $c || exit 1 ;;
+    sweep*)
+      # sweep<C>[f]:T1,T2,...  shading thresholds (tools/sweep_threshold.sh; -1 = the default)
+      c=${step:5:1}; ts=$(echo ${step#*:} | tr , ' '); f=""; fo=""
+      [ "${step:6:1}" = "f" ] && { f=f; fo="--bsp-cull 2"; }
+      case $c in 3) o="";; 4) o="--config 4";; 5) o="--config 5 --spp 128";; 2) o="--config 2";; esac
+      bash tools/sweep_threshold.sh $OUT/sweep_c$c$f.txt "$o $fo" $ts || { tail -5 $OUT/sweep_c$c$f.txt; exit 1; }
+      cat $OUT/sweep_c$c$f.txt ;;
+    stress)
+      # whole frames of configs 3/4/5 at their BASELINE spp in every culling mode (tools/cull_stress.py)
+      timeout -k 10 900 python -u tools/cull_stress.py > $OUT/cull_stress.txt 2>&1 || { echo "cull_stress rc=$?"; tail -20 $OUT/cull_stress.txt; exit 1; }
+      grep -E "differ" $OUT/cull_stress.txt ;;
     m3) bash tools/measure.sh $TAG/c3 || exit 1 ;;
     m3fast) bash tools/measure.sh $TAG/c3fast --bsp-cull 2 || exit 1 ;;
     m4) bash tools/measure.sh $TAG/c4 --config 4 --no-cpu-baseline || exit 1 ;;

@@ -101,7 +101,9 @@ void walk_sim_lost(double* o) { for (int i = 0; i < 4; i++) o[i] = g_lost[i]; }
  * (the eye's distance from their planes) left out; a camera-ray cull that only those
  * triangles prevent tests them directly with the ray's interval (a second load and
  * up to k tests) and culls when none is accepted -- exact by the same argument */
-static int g_camx = 0, g_use_hx = 0;
+static const Scene* g_scene = 0;
+static int g_camx = 0, g_use_hx = 0, g_camx_bound = 0;
+void walk_sim_camx_bound(int b) { g_camx_bound = b; }
 static double* g_hx = 0;     /* per node: the (k+1)-th smallest H of the subtree */
 static uint32_t* g_xt = 0;   /* per node: its k excluded triangles (~0u: none) */
 static const uint32_t* g_tree_x = 0;
@@ -169,6 +171,9 @@ static double cert_margin_c(const double* c, v3 o, v3 d, const float* b)
         hi += p < q ? q : p;
     }
     double dlb = lo > 0 ? lo : (hi < 0 ? -hi : 0);
+    static int nocone = -1;
+    if (nocone < 0) { const char* e = getenv("WALK_NOCONE"); nocone = e ? atoi(e) : 0; }
+    if (nocone) dlb = 0;
     double den = 2 * dlb - 32 * u * w1;
     double fl = 1e-10 / E2;
     if (g_cert_floor_only || den < fl) den = fl;
@@ -180,8 +185,25 @@ static double cert_margin_c(const double* c, v3 o, v3 d, const float* b)
             Dinf = fmax(Dinf, fmax(a, e));
         }
         const size_t nd = c - g_cert >= 0 && (c - g_cert) % 7 == 0 ? (c - g_cert) / 7 : 0;
-        double H = g_use_hx ? g_hx[nd] : g_hcam[nd];
+        double H = (g_use_hx || g_camx_bound) ? g_hx[nd] : g_hcam[nd];
         double dc = winf * (H - 128 * u * d1) / Dinf;
+        if (g_camx_bound && g_camx) {
+            /* the excluded triangles' own |w . n*| / E_T^2, per ray (their normals stored
+             * in the treelet): the camera bound holds for the rest of the subtree */
+            for (int j = 0; j < g_camx; j++) {
+                uint32_t t = g_xt[nd * CAMX_MAX + j];
+                if (t == ~0u) continue;
+                const uint32_t* ix = g_scene->idx + 4 * (size_t)t;
+                v3 p0 = V(g_scene->pos[4 * ix[0]], g_scene->pos[4 * ix[0] + 1], g_scene->pos[4 * ix[0] + 2]);
+                v3 p1 = V(g_scene->pos[4 * ix[1]], g_scene->pos[4 * ix[1] + 1], g_scene->pos[4 * ix[1] + 2]);
+                v3 p2 = V(g_scene->pos[4 * ix[2]], g_scene->pos[4 * ix[2] + 1], g_scene->pos[4 * ix[2] + 2]);
+                v3 e0 = sub(p1, p0), e1 = sub(p2, p0);
+                double nn[3] = {(double)e0.y * e1.z - (double)e0.z * e1.y, (double)e0.z * e1.x - (double)e0.x * e1.z,
+                                (double)e0.x * e1.y - (double)e0.y * e1.x};
+                double wn = fabs(d.x * nn[0] + d.y * nn[1] + d.z * nn[2]) / E2 - 24 * u * w1;
+                if (wn < dc) dc = wn;
+            }
+        }
         if (dc > den) den = dc;
     }
     if (g_hy && d.x == 0.0f && d.y == 1.0f && d.z == 0.0f) {
@@ -219,7 +241,6 @@ static int cell_clip(uint32_t node, v3 o, v3 d, double* t0p, double* t1p)
     *t1p = t1;
     return t0 > t1 + (fabs(t0) + fabs(t1)) * 0x1p-18;
 }
-static const Scene* g_scene = 0;
 static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
 {
     const float* b = g_boxes + 6 * (size_t)node;
@@ -244,7 +265,7 @@ static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
         g_tn = (float)t0;
         g_tf = (float)t1;
         int miss = t0 > t1 + (fabs(t0) + fabs(t1)) * 0x1p-18;
-        if (!miss && g_camx && g_hcam && o.x == g_eye.x && o.y == g_eye.y && o.z == g_eye.z && isfinite(g_hx[node])) {
+        if (!miss && g_camx && !g_camx_bound && g_hcam && o.x == g_eye.x && o.y == g_eye.y && o.z == g_eye.z && isfinite(g_hx[node])) {
             g_use_hx = 1;
             const double m2 = cert_margin(node, o, d, b);
             g_use_hx = 0;

@@ -219,6 +219,7 @@ def main():
                 hn_c = np.ascontiguousarray(hn)
                 L.walk_sim_camx(P(tree.ctypes.data), P(ids.ctypes.data), ctypes.c_uint32(n), P(hn_c.ctypes.data),
                                 int(os.environ["WALK_CAMX"]))
+                L.walk_sim_camx_bound(int(os.environ.get("WALK_CAMX_BOUND", "0")))
             L.walk_sim_cam.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
             L.walk_sim_cam(hcam.ctypes.data, *[float(x) for x in eye])
     L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
