@@ -56,17 +56,20 @@ def test_cornell_w7e3_full_frame(rt):
     # the whole config-2 frame (1024 x 1024) at 8 spp: flat, coplanar walls and
     # the area-light shadow rays that graze the ceiling the light sits in
     s = Scene(rt, rt.Mesh.from_obj(model("CornellBoxWithBlocks.obj")), "BSP")
-    _all_same(_frames(rt, s, "W7E3", CORNELL_CAM, 1024, 1024, (0, 0, 1024, 1024), 8))
+    off, on, fast, sil = _frames(rt, s, "W7E3", CORNELL_CAM, 1024, 1024, (0, 0, 1024, 1024), 8)
+    _all_same((off, on, fast, sil))
     assert on[2]["tri_tests"] <= off[2]["tri_tests"]
     s.ctx.close()
 
 
 def test_bunny_w9e1_frame(rt):
     s = Scene(rt, rt.Mesh.synth_bunny(), "BSP", env=(0.8, 0.9, 1.0))
-    _all_same(_frames(rt, s, "W9E1", BUNNY_CAM, 1920, 1080, (0, 0, 1920, 1080), 2))
+    off, on, fast, sil = _frames(rt, s, "W9E1", BUNNY_CAM, 1920, 1080, (0, 0, 1920, 1080), 2)
+    _all_same((off, on, fast, sil))
     # the point of it: far fewer nodes and triangles
     assert on[2]["node_interior"] < 0.75 * off[2]["node_interior"]
     assert fast[2]["node_interior"] < 0.6 * off[2]["node_interior"]
+    assert sil[2]["node_interior"] <= 1.01 * on[2]["node_interior"]   # (a tighter camera bound)
     s.ctx.close()
 
 
