@@ -6,10 +6,12 @@
 #   tests [pytest args]   the GPU suite (or the named test files: tests:file1,file2)
 #   ab<C>[f]:<v1>,<v2>,.. A/B of variants/<v>/lib02562rt.so on config C (2, 3, 4; 5 at 128 spp;
 #                         f: the fast margin)
-#   m<C>[fast]            bench line + kernel-trace stats + PMC passes (tools/measure.sh)
+#   m<C>[fast] / m4sil    bench line + kernel-trace stats + PMC passes (tools/measure.sh)
+#   n2 / n4 / n8          the same for rank 0's share of an N-rank split (bench.py --rank-share N)
 #   wf<C>[f] / wfpmc<C>   the wavefront split's price (tools/wavefront_price.py) / its PMC passes
 #   stress                tools/cull_stress.py: configs 3-5 whole frames, every culling mode
 #   sweep<C>[f]:T1,..     shading-threshold sweep (tools/sweep_threshold.sh)
+#   scale<C>              tools/scale_probe.py: each rank's share of the N-rank split, N = 1, 2, 4, 8
 set -u
 TAG=$1; shift
 export TMPDIR=/tmp
@@ -45,6 +47,11 @@ for step in "$@"; do
       case $c in 3) o="";; 4) o="--config 4";; 5) o="--config 5 --spp 128";; 2) o="--config 2";; esac
       bash tools/sweep_threshold.sh $OUT/sweep_c$c$f.txt "$o $fo" $ts || { tail -5 $OUT/sweep_c$c$f.txt; exit 1; }
       cat $OUT/sweep_c$c$f.txt ;;
+    scale3|scale4|scale5)
+      # per-rank shares of the N-rank tile split, timed one at a time (tools/scale_probe.py)
+      c=${step:5:1}; w=""; [ $c = 5 ] && w="--warm 0"
+      timeout -k 10 600 python tools/scale_probe.py --config $c $w > $OUT/scale_c$c.txt 2>&1 || { echo "scale_probe rc=$?"; tail -5 $OUT/scale_c$c.txt; exit 1; }
+      tail -6 $OUT/scale_c$c.txt ;;
     stress)
       # whole frames of configs 3/4/5 at their BASELINE spp in every culling mode (tools/cull_stress.py)
       timeout -k 10 900 python -u tools/cull_stress.py > $OUT/cull_stress.txt 2>&1 || { echo "cull_stress rc=$?"; tail -20 $OUT/cull_stress.txt; exit 1; }
@@ -56,6 +63,8 @@ for step in "$@"; do
     m5) bash tools/measure.sh $TAG/c5 --config 5 --no-cpu-baseline || exit 1 ;;
     m5fast) bash tools/measure.sh $TAG/c5fast --config 5 --no-cpu-baseline --bsp-cull 2 || exit 1 ;;
     m2) bash tools/measure.sh $TAG/c2 --config 2 --no-cpu-baseline || exit 1 ;;
+    m4sil) bash tools/measure.sh $TAG/c4sil --config 4 --no-cpu-baseline --bsp-cull 3 || exit 1 ;;
+    n2|n4|n8) bash tools/measure.sh $TAG/c3$step --no-cpu-baseline --rank-share ${step#n} || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
