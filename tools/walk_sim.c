@@ -331,7 +331,7 @@ static uint32_t depth_of(uint32_t n0) { uint32_t m = n0 + 1, d = 0; while (m > 1
 
 /* stats[variant][k]: 0 walk trips, 1 leaf trips, 2 interior decisions, 3 leaf visits,
  * 4 empty leaf visits, 5 tests, 6 pushes, 7 pops, 8 hits, 9 mismatches vs v0 */
-enum { S_WT, S_LT, S_DEC, S_LEAF, S_EMPTY, S_TEST, S_PUSH, S_POP, S_HIT, S_BAD, S_N };
+enum { S_WT, S_LT, S_DEC, S_LEAF, S_EMPTY, S_TEST, S_PUSH, S_POP, S_HIT, S_BAD, S_BOXT, S_N };
 
 static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int anyhit, float* hd, uint32_t* htri,
                 double* st)
@@ -346,12 +346,16 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
         st[S_WT] += 1;
         int lv = 0, reached_leaf = 0, do_pop = 0;
         float ctn = -INFINITY, ctf = INFINITY;   /* v4 + WALK_CLIP: decisions against the box's interval */
-        if (var >= 3 && g_boxes && (node == 0 || !g_root_only) && box_miss(node, o, d, tmin, tmax)) {
+        static int box_every = -1;
+        if (box_every < 0) { const char* e = getenv("WALK_BOX_EVERY"); box_every = e ? atoi(e) : 1; }
+        const int test_box = box_every <= 1 || ((depth_of(node) / 3) % (uint32_t)box_every) == 0;
+        if (var >= 3 && g_boxes && test_box) st[S_BOXT] += 1;
+        if (var >= 3 && g_boxes && test_box && (node == 0 || !g_root_only) && box_miss(node, o, d, tmin, tmax)) {
             do_pop = 1;   /* v3: the subtree's content misses the ray interval */
             g_cull[depth_of(node) < 32 ? depth_of(node) : 31] += 1;
             g_cull_leaf += (s->tree[4 * node] & 3u) == 3u;
             lv = g_levels;
-        } else if (var == 4 && g_boxes && g_clip) {
+        } else if (var == 4 && g_boxes && g_clip && test_box) {
             ctn = g_tn;
             ctf = g_tf;
         }

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import oracle_ffi as O  # noqa: E402
 
 NAMES = ["walk_trips", "leaf_trips", "decisions", "leaf_visits", "empty_leaves", "tests", "pushes", "pops", "hits",
-         "mismatch"]
+         "mismatch", "box_tests"]
 
 
 def lib():
@@ -100,7 +100,7 @@ def main():
                 i += 1
         keep = kind == int(os.environ["WALK_RAYS"])
         R, F = np.ascontiguousarray(R[keep]), np.ascontiguousarray(F[keep])
-    out = np.zeros(50, np.float64)
+    out = np.zeros(55, np.float64)
     # content boxes of every node's subtree (v3), bottom-up from the leaves' triangles
     boxes = None
     if os.environ.get("WALK_BOXES"):
@@ -233,7 +233,7 @@ def main():
     L.walk_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
                P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
                P(out.ctypes.data))
-    out = out.reshape(5, 10)
+    out = out.reshape(5, 11)
     ks = np.array([4, 6, 8, 10, 12, 16], np.uint32)
     tr = np.zeros(4 * len(ks), np.float64)
     L.trail_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
@@ -273,6 +273,7 @@ def main():
     for v in range(5 if boxes is not None else 3):
         s = {k: round(out[v, i] / len(R), 3) for i, k in enumerate(NAMES)}
         s["mismatch"] = int(out[v, 9])
+        s["box_tests"] = round(out[v, 10] / len(R), 3)
         tr = out[v, 0] + out[v, 1]
         print(f"v{v}", s, "trips/ray", round(tr / len(R), 3), "vs v0", round(tr / (out[0, 0] + out[0, 1]), 4))
 
