@@ -876,7 +876,19 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     if constexpr (CM == 2) {
         const __amdgpu_buffer_rsrc_t rs6 = __builtin_amdgcn_make_buffer_rsrc(
             (void*)S.bsp_sil, (short)0, (int)((S.bsp_bytes / BSP_TREELET_BYTES) * 16u), 0x00020000);
-        q6 = __builtin_amdgcn_raw_buffer_load_b128(rs6, t.node * 16u, 0, 0);
+        // only a walking camera ray uses it: every other lane's offset lies past the
+        // array, so its load returns zeros without a memory access (zeros give
+        // dc = dcam, and a non-camera ray ignores dc) -- the secondary rays of a
+        // large scene do not stream the array
+        uint32_t off6 = t.node * 16u;
+#ifndef RT_SIL_MASKED
+#define RT_SIL_MASKED 1
+#endif
+        if (RT_SIL_MASKED) {
+            const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
+            off6 = (!in_leaf & cam) ? off6 : 0x80000000u;
+        }
+        q6 = __builtin_amdgcn_raw_buffer_load_b128(rs6, off6, 0, 0);
         asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6));
     } else {
         asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5));
