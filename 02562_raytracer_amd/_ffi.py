@@ -33,7 +33,7 @@ RT_OPT_SAMPLE_BUDGET_MB = 5
 RT_OPT_UNIT_ORDER = 6
 RT_OPT_BSP_CULL = 9
 RT_OPT_ASYNC_FOLD = 10
-RT_BSP_CULL_OFF, RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_FAST, RT_BSP_CULL_SILHOUETTE = range(4)
+RT_BSP_CULL_OFF, RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_FAST, RT_BSP_CULL_SILHOUETTE, RT_BSP_CULL_AUTO = range(5)
 BSP_TREELET_BYTES = 96   # rt_internal.h: the BSP walk's treelet (rt_download_bsp_treelets)
 RT_OPT_KERNEL_TIMING = 7
 RT_COMM_ID_BYTES = 128
@@ -132,6 +132,7 @@ SIGNATURES = {
     "rt_get_stream": (vp, [vp]),
     "rt_synchronize": (C.c_int, [vp]),
     "rt_set_option": (C.c_int, [vp, C.c_int, C.c_int64]),
+    "rt_bsp_cull_in_use": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_float)]),
     "rt_last_error": (C.c_char_p, [vp]),
     "rt_device_alloc": (C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
     "rt_device_free": (C.c_int, [vp, vp]),

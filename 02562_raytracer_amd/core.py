@@ -261,6 +261,14 @@ class Context:
     def set_option(self, opt, value):
         self._chk(F.lib().rt_set_option(self._h, opt, int(value)))
 
+    def bsp_cull_in_use(self):
+        """(mode, certified probe ms, silhouette probe ms): the culling mode the BSP
+        kernels run now (rt_bsp_cull_in_use; RT_BSP_CULL_AUTO's choice once probed)."""
+        m = C.c_int()
+        ms = (C.c_float * 2)()
+        self._chk(F.lib().rt_bsp_cull_in_use(self._h, C.byref(m), ms))
+        return m.value, ms[0], ms[1]
+
     def upload_mesh(self, mesh):
         self._chk(F.lib().rt_upload_mesh_host(self._h, mesh.handle))
 

@@ -72,7 +72,7 @@ struct rt_ctx {
     int shade_threshold = -1;   // -1: per walk (BSP 8, BVH 4); pixel-major units refill together (coherent samples)
     uint32_t sample_chunk = 1;          // iterations per k_path work unit
     uint32_t unit_order = 1;            // 0: chunk-major, 1: pixel-major
-    uint32_t bsp_cull = RT_BSP_CULL_CERTIFIED;   // RT_OPT_BSP_CULL: subtree culling by content boxes in the BSP walk
+    uint32_t bsp_cull = RT_BSP_CULL_AUTO;   // RT_OPT_BSP_CULL: subtree culling by content boxes in the BSP walk
     float bsp_scale = 0.0f;             // the scene's coordinate magnitude (set on upload; the margins' scale)
     uint64_t sample_budget_mb = 16384;  // per-sample scratch (one pass at 1080p x 256 spp needs 8.1 GiB)
     DevBuf samples;
@@ -97,6 +97,11 @@ struct rt_ctx {
     float hcam_eye[3] = {0, 0, 0};
     DevBuf hcam_scratch;
     DevBuf bsp_sil;   // RT_BSP_CULL_SILHOUETTE's node data ((nnodes + 1) x 16 B)
+    // RT_BSP_CULL_AUTO: the certified form the W9E1 walk runs for this scene and eye
+    // (0: not probed yet; reset with the camera terms), and the probe's timings
+    uint32_t auto_cull = 0;
+    float auto_ms[2] = {0, 0};
+    hipEvent_t auto_ev[8] = {};
     DevBuf bvh_nodes, bvh_ids;   // bvh_nodes: [32-B nodes | 48-B records]
     DevBuf bvh_ref;              // the GpuNode array in the reference layout (rt_download_bvh)
     uint32_t bvh_rec_off = 0;
@@ -301,6 +306,8 @@ void rt_destroy(rt_ctx* c)
     for (hipEvent_t e : c->gev) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
+    for (hipEvent_t e : c->auto_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -349,8 +356,8 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
         c->ktiming = value != 0;
         return RT_OK;
     case RT_OPT_BSP_CULL:
-        if (value < RT_BSP_CULL_OFF || value > RT_BSP_CULL_SILHOUETTE)
-            return fail(c, RT_E_INVALID, "BSP cull must be RT_BSP_CULL_OFF, _CERTIFIED, _FAST or _SILHOUETTE");
+        if (value < RT_BSP_CULL_OFF || value > RT_BSP_CULL_AUTO)
+            return fail(c, RT_E_INVALID, "BSP cull must be RT_BSP_CULL_OFF, _CERTIFIED, _FAST, _SILHOUETTE or _AUTO");
         c->bsp_cull = (uint32_t)value;
         return RT_OK;
     case RT_OPT_UNIT_ORDER:
@@ -767,6 +774,24 @@ int rt_download_bsp(rt_ctx* c, uint32_t* tree, float* planes, uint32_t cap_nodes
 }
 
 static int ensure_hcam(rt_ctx* c);
+
+// the culling modes whose margin is the certified bound (their treelets carry the camera terms)
+static bool cull_certified(const rt_ctx* c)
+{
+    return c->bsp_cull == RT_BSP_CULL_CERTIFIED || c->bsp_cull == RT_BSP_CULL_SILHOUETTE ||
+           c->bsp_cull == RT_BSP_CULL_AUTO;
+}
+
+// the mode the BSP kernels run: the silhouette bound needs its node data, made with the
+// camera terms (ensure_hcam), so without them (no uniforms, or a non-finite eye) it runs
+// the certified kernel; RT_BSP_CULL_AUTO runs its probe's choice (certified until probed)
+static uint32_t cull_in_use(const rt_ctx* c)
+{
+    if (c->bsp_cull == RT_BSP_CULL_SILHOUETTE) return c->hcam_valid ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
+    if (c->bsp_cull == RT_BSP_CULL_AUTO)
+        return c->hcam_valid && c->auto_cull == RT_BSP_CULL_SILHOUETTE ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
+    return c->bsp_cull;
+}
 int rt_download_bsp_treelets(rt_ctx* c, void* dst, uint64_t cap_bytes, uint64_t* bytes)
 {
     if (!c) return RT_E_INVALID;
@@ -905,8 +930,7 @@ int rt_set_environment_map(rt_ctx* c, const uint8_t* rgba8, uint32_t width, uint
 // rt_bsp_build.hip launch_bsp_camera): recomputed when the eye moves.
 static int ensure_hcam(rt_ctx* c)
 {
-    if (!c->has_bsp || !c->has_u || (c->bsp_cull != RT_BSP_CULL_CERTIFIED && c->bsp_cull != RT_BSP_CULL_SILHOUETTE))
-        return RT_OK;
+    if (!c->has_bsp || !c->has_u || !cull_certified(c)) return RT_OK;
     const float* e = c->u.camera_pos;
     if (c->hcam_valid && memcmp(e, c->hcam_eye, sizeof c->hcam_eye) == 0) return RT_OK;
     if (!(std::isfinite(e[0]) && std::isfinite(e[1]) && std::isfinite(e[2]))) return RT_OK;
@@ -919,6 +943,7 @@ static int ensure_hcam(rt_ctx* c)
         return fail(c, RT_E_DEVICE, "BSP camera terms: launch failed");
     memcpy(c->hcam_eye, e, sizeof c->hcam_eye);
     c->hcam_valid = true;
+    c->auto_cull = 0;   // (RT_BSP_CULL_AUTO probes again for the new eye)
     return RT_OK;
 }
 
@@ -943,10 +968,7 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bsp_ids = c->bsp_ids.as<uint32_t>();
     S.bsp_tm = c->bsp_tm.as<uint2>();
     S.bsp_sil = c->bsp_sil.as<uint4>();
-    // the silhouette mode needs its node data, made with the camera terms (ensure_hcam);
-    // without them (no uniforms, or a non-finite eye) it runs the certified kernel
-    S.bsp_cull_mode = c->bsp_cull == RT_BSP_CULL_SILHOUETTE && !c->hcam_valid ? (uint32_t)RT_BSP_CULL_CERTIFIED
-                                                                                : (uint32_t)c->bsp_cull;
+    S.bsp_cull_mode = cull_in_use(c);
     S.bsp_depth = c->bsp_depth;
     memcpy(S.aabb, c->aabb, sizeof S.aabb);
     S.bvh_base = c->bvh_nodes.as<uint8_t>();
@@ -959,7 +981,7 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bsp_cull_emax = c->bsp_cull != RT_BSP_CULL_OFF ? FLT_MAX : INFINITY;
     // off: the fast formula's constants (k1 = 0 picks k_path's fast-margin
     // instantiation, launch_path); the +inf gap culls nothing either way
-    if (c->bsp_cull != RT_BSP_CULL_CERTIFIED && c->bsp_cull != RT_BSP_CULL_SILHOUETTE) {
+    if (!cull_certified(c)) {
         S.cull_k1 = 0.0f;
         S.cull_k3 = 0.0f;
         S.cull_ko = 0x1p-10f;
@@ -1050,6 +1072,59 @@ int rt_trace_rays(rt_ctx* c, rt_traverse trav, const float* rays, const uint32_t
     return RT_OK;
 }
 
+// RT_BSP_CULL_AUTO: times the certified and the silhouette W9E1 kernels on a probe of
+// the render about to run -- its first iterations over the whole region, at most 2^25
+// samples, written to the per-sample scratch only (no fold: accum and ids are
+// untouched) -- twice each, alternating, and keeps the faster for this scene and eye.
+// Both are exact (the same frame bit for bit), so the choice moves only time: the
+// silhouette bound gains 15 % on config 4's far grid of bunnies and loses 3-4 % on
+// configs 3 and 5.  L: the render's launch with its scratch and
+// stride set; max_spp: the iterations that scratch holds.
+static int probe_auto_cull(rt_ctx* c, rtk::DevScene& S, const rtk::DevLaunch& L, uint32_t max_spp, rt_mode mode,
+                           rt_traverse trav)
+{
+    rtk::DevLaunch P = L;
+    const uint64_t cap = std::max<uint64_t>(1, (1ull << 25) / std::max<uint32_t>(1, L.stride));
+    P.spp = (uint32_t)std::min<uint64_t>({(uint64_t)L.spp, (uint64_t)max_spp, cap});
+    P.chunk = 1;
+    P.nchunks = P.spp;
+    P.unit_order = c->unit_order;
+    for (hipEvent_t& e : c->auto_ev)
+        if (!e) HIPCHK(c, hipEventCreate(&e));
+    const uint32_t order[4] = {RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_SILHOUETTE, RT_BSP_CULL_CERTIFIED,
+                               RT_BSP_CULL_SILHOUETTE};
+    for (int i = 0; i < 4; i++) {
+        S.bsp_cull_mode = order[i];
+        HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
+        HIPCHK(c, hipEventRecord(c->auto_ev[2 * i], c->stream));
+        const int r = rtk::launch_render(S, P, mode, trav, false, c->num_cus, c->waves_per_cu, c->stream);
+        if (r) return fail(c, r, std::string("culling probe launch failed: ") + hipGetErrorString(hipGetLastError()));
+        HIPCHK(c, hipEventRecord(c->auto_ev[2 * i + 1], c->stream));
+    }
+    HIPCHK(c, hipEventSynchronize(c->auto_ev[7]));
+    float t[4];
+    for (int i = 0; i < 4; i++) HIPCHK(c, hipEventElapsedTime(&t[i], c->auto_ev[2 * i], c->auto_ev[2 * i + 1]));
+    c->auto_ms[0] = std::min(t[0], t[2]);
+    c->auto_ms[1] = std::min(t[1], t[3]);
+    c->auto_cull = c->auto_ms[1] < c->auto_ms[0] ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
+    S.bsp_cull_mode = cull_in_use(c);
+    // the render's ray counts are its own: clear what the probe's launches counted
+    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
+    return RT_OK;
+}
+
+int rt_bsp_cull_in_use(rt_ctx* c, int* mode, float* probe_ms)
+{
+    if (!c || !mode) return RT_E_INVALID;
+    *mode = (int)cull_in_use(c);
+    if (probe_ms) {
+        const bool probed = c->bsp_cull == RT_BSP_CULL_AUTO && c->auto_cull != 0;
+        probe_ms[0] = probed ? c->auto_ms[0] : 0.0f;
+        probe_ms[1] = probed ? c->auto_ms[1] : 0.0f;
+    }
+    return RT_OK;
+}
+
 static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaunch& L, rt_ray_counts* counts)
 {
     if (!c->has_u) return fail(c, RT_E_NOT_READY, "rt_render: uniforms not set");
@@ -1077,7 +1152,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // itself, so a fold of an earlier path render still pending there is joined first
     if (int r = path ? set_dev_nojoin(c) : set_dev(c)) return r;
     if (int r = ensure_hcam(c)) return r;
-    const rtk::DevScene S = dev_scene(c);
+    rtk::DevScene S = dev_scene(c);
     L.u = c->u;
     rtk::camera_basis(c->u, L.cam);
     L.jitter = c->has_jitter ? c->jitter.as<float>() : nullptr;
@@ -1107,9 +1182,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // nodes and its rays take more trips, so finished lanes wait longer for the last
     // ones: 16 and 32 (profiles/r04/sweep_T.txt: config 3 fixed 16 +1.9 % over 8,
     // config 4 16..24 +3 %, config 5 32 +1.1 %).
-    const uint32_t adaptive = c->bsp_cull == RT_BSP_CULL_CERTIFIED || c->bsp_cull == RT_BSP_CULL_SILHOUETTE
-                                  ? (1u << 16) | (32u << 8) | 16u
-                                                                   : (1u << 16) | (24u << 8) | 8u;
+    const uint32_t adaptive = cull_certified(c) ? (1u << 16) | (32u << 8) | 16u : (1u << 16) | (24u << 8) | 8u;
     L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold
                                    : trav == RT_TRAVERSE_BVH ? 4
                                    : mode == RT_MODE_W7E3    ? 24
@@ -1133,6 +1206,11 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
         if (c->samples.n < need) HIPCHK(c, c->samples.alloc(need));
         if (async && c->samples2.n < need) HIPCHK(c, c->samples2.alloc(need));
         L.samples = c->samples.as<float4>();
+        if (mode == RT_MODE_W9E1 && trav == RT_TRAVERSE_BSP && c->bsp_cull == RT_BSP_CULL_AUTO && c->hcam_valid &&
+            c->auto_cull == 0) {
+            if (int r = set_dev(c)) return r;   // (a pending fold may still read the scratch)
+            if (int r = probe_auto_cull(c, S, L, pass_spp, mode, trav)) return r;
+        }
         if (async) {   // the folds follow the context stream's work up to here
             HIPCHK(c, hipEventRecord(c->ev_enter, c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fold_stream, c->ev_enter, 0));

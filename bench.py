@@ -214,8 +214,8 @@ def main():
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)
     ap.add_argument("--bsp-cull", type=int, default=None,
-                    help="RT_OPT_BSP_CULL: 0 off, 1 certified (the library default), 2 fast margin, "
-                         "3 certified + silhouette bound")
+                    help="RT_OPT_BSP_CULL: 0 off, 1 certified, 2 fast margin, 3 certified + silhouette bound, "
+                         "4 the faster of 1 and 3 by a timed probe (the library default)")
     ap.add_argument("--async-fold", action="store_true",
                     help="pipelined frames (RT_OPT_ASYNC_FOLD 1): a frame's fold and gather overlap the next "
                          "frame's traversal kernel (measured slower on config 3: profiles/r04/ab_async_fold.txt)")
@@ -419,8 +419,16 @@ def main():
         # one GPU -- rank 0's, with rank 0's own kernel time and the PMC summary of
         # rank 0's share (profiles/pmc_summary.json key _n<N>, measured with --rank-share N)
         bytes_per_launch = rays[4] / (world if use_dist else 1) / max(1, launches_per_step)
-        cull = args.bsp_cull if args.bsp_cull is not None else rt._ffi.RT_BSP_CULL_CERTIFIED
-        cull_name = {0: "off", 1: "certified", 2: "fast", 3: "silhouette"}[cull] if trav == "BSP" else None
+        # the culling mode the kernel ran (RT_BSP_CULL_AUTO: its probe's choice, made in
+        # the first warm-up step) picks the instantiation and the PMC summary
+        names = {0: "off", 1: "certified", 2: "fast", 3: "silhouette"}
+        if hasattr(rt._ffi.lib(), "rt_bsp_cull_in_use"):
+            cull, probe_c, probe_s = ctx.bsp_cull_in_use()
+        else:   # (an A/B variant of an earlier tree)
+            cull, probe_c, probe_s = args.bsp_cull if args.bsp_cull is not None else rt._ffi.RT_BSP_CULL_CERTIFIED, 0, 0
+        cull_name = names[cull] if trav == "BSP" else None
+        if trav == "BSP" and probe_c > 0:
+            cull_name = f"auto: {cull_name} (probe: certified {probe_c:.2f} ms, silhouette {probe_s:.2f} ms)"
         roof = roofline(pmc_key(W, H, spp, trav, nsplit, args.config, cull), kern_ms_own, bytes_per_launch, args.config,
                         f"k_path<{wl.mode},{trav}>")
         roof["launches_per_step"] = launches_per_step

@@ -188,7 +188,7 @@ typedef struct rt_ray_counts {
                                      that box.  One of RT_BSP_CULL_*: */
 #define RT_BSP_CULL_OFF        0  /* every node of bsp.wgsl's walk is visited: the reference's walk and tested-
                                      triangle sequence, by construction */
-#define RT_BSP_CULL_CERTIFIED  1  /* (default) the margin is a proven bound on how far an f32 accept of
+#define RT_BSP_CULL_CERTIFIED  1  /* the margin is a proven bound on how far an f32 accept of
                                      intersect_triangle (w7e3.wgsl:286-332) can lie from its triangle's box, from the
                                      subtree's largest edge, its box of normals and, for rays that start at the
                                      uniforms' camera eye, its per-eye plane distance: every hit (triangle, distance,
@@ -203,8 +203,13 @@ typedef struct rt_ray_counts {
                                      camera rays: each subtree's two triangles nearest the eye's plane-distance
                                      floor (its silhouette) are bounded per ray by their own normals, the rest by
                                      their camera term.  Fewer trips for far, many-object views (config 4: +15 %),
-                                     more arithmetic per trip (config 3: -4 %, config 5: -6 %): opt-in.  The W9E1
+                                     more arithmetic per trip (config 3: -4 %, config 5: -3 %).  The W9E1
                                      path kernel and rt_trace_batch use it; other kernels run the certified form */
+#define RT_BSP_CULL_AUTO       4  /* (default) exact as RT_BSP_CULL_CERTIFIED: the first W9E1 BSP render for a scene and eye
+                                     times the certified and the silhouette kernels on a probe of itself (its first
+                                     iterations, at most 2^25 samples, into the per-sample scratch only; accum and
+                                     ids untouched; two launches each) and runs the faster from then on, until the
+                                     BSP or the eye changes.  rt_bsp_cull_in_use reports the choice */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
 
@@ -225,6 +230,13 @@ void* rt_get_stream(rt_ctx* ctx);
 int rt_synchronize(rt_ctx* ctx);
 
 int rt_set_option(rt_ctx* ctx, int option, int64_t value);
+
+/* The culling mode the BSP kernels run now (RT_BSP_CULL_*): the option's value, except
+ * that RT_BSP_CULL_SILHOUETTE without the eye's camera terms runs CERTIFIED and
+ * RT_BSP_CULL_AUTO runs its probe's choice (CERTIFIED or SILHOUETTE; CERTIFIED until
+ * the probe has run for the current BSP and eye).  probe_ms (2 floats, or NULL): the
+ * probe's best certified and silhouette launch times, 0 when it has not run. */
+int rt_bsp_cull_in_use(rt_ctx* ctx, int* mode, float* probe_ms);
 
 /* Message describing the last failure on this context (or the last
  * context-less failure when ctx == NULL).  Never NULL. */

@@ -1,7 +1,8 @@
 """Subtree culling of the BSP walk (RT_OPT_BSP_CULL, rt_kernels.hip bsp_box_miss;
 DESIGN.md section 4 "Subtree culling") changes only the work, never the result:
 frames rendered with certified culling (the default; exact by proof), with the
-fast margin (RT_BSP_CULL_FAST) and with culling off (every node of
+silhouette bound and the timed choice between the two (RT_BSP_CULL_SILHOUETTE,
+RT_BSP_CULL_AUTO), with the fast margin (RT_BSP_CULL_FAST) and with culling off (every node of
 bsp.wgsl:10-81 visited) are equal bit for bit -- radiance, primary-hit ids and
 the ray counts --
 across the shaders and walks that use the BSP: the path tracers (W7E3, W9E1 with
@@ -19,7 +20,7 @@ from parity_util import BUNNY_CAM, CORNELL_CAM, TEAPOT_CAM, Scene
 pytestmark = pytest.mark.gpu
 
 
-CULL_MODES = (0, 1, 2, 3)   # RT_BSP_CULL_OFF, _CERTIFIED (default), _FAST, _SILHOUETTE
+CULL_MODES = (0, 1, 2, 3, 4)   # RT_BSP_CULL_OFF, _CERTIFIED (default), _FAST, _SILHOUETTE, _AUTO
 
 
 def _frames(rt, s, mode, cam, W, H, region, spp, selection1=0, jitter=None):
@@ -30,7 +31,7 @@ def _frames(rt, s, mode, cam, W, H, region, spp, selection1=0, jitter=None):
         out.append(s.render_gpu(mode, cam, W, H, region, 0, spp, selection1=selection1, jitter=jitter))
     s.ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, rt._ffi.RT_BSP_CULL_CERTIFIED)
     s.ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
-    for f, name in zip(out[1:], ("certified", "fast", "silhouette")):
+    for f, name in zip(out[1:], ("certified", "fast", "silhouette", "auto")):
         print(f"{mode}: {name} culls {f[2]['subtree_culls']}, interior nodes "
               f"{f[2]['node_interior'] / max(1, out[0][2]['node_interior']):.3f} of the unculled walk")
     return out
@@ -47,7 +48,7 @@ def _same(a, b, culled=True):
 
 
 def _all_same(frames, culled=True):
-    off, *ons = frames   # certified, fast, silhouette
+    off, *ons = frames   # certified, fast, silhouette, auto
     for on in ons:
         _same(off, on, culled)
 
@@ -56,16 +57,16 @@ def test_cornell_w7e3_full_frame(rt):
     # the whole config-2 frame (1024 x 1024) at 8 spp: flat, coplanar walls and
     # the area-light shadow rays that graze the ceiling the light sits in
     s = Scene(rt, rt.Mesh.from_obj(model("CornellBoxWithBlocks.obj")), "BSP")
-    off, on, fast, sil = _frames(rt, s, "W7E3", CORNELL_CAM, 1024, 1024, (0, 0, 1024, 1024), 8)
-    _all_same((off, on, fast, sil))
+    off, on, fast, sil, auto = _frames(rt, s, "W7E3", CORNELL_CAM, 1024, 1024, (0, 0, 1024, 1024), 8)
+    _all_same((off, on, fast, sil, auto))
     assert on[2]["tri_tests"] <= off[2]["tri_tests"]
     s.ctx.close()
 
 
 def test_bunny_w9e1_frame(rt):
     s = Scene(rt, rt.Mesh.synth_bunny(), "BSP", env=(0.8, 0.9, 1.0))
-    off, on, fast, sil = _frames(rt, s, "W9E1", BUNNY_CAM, 1920, 1080, (0, 0, 1920, 1080), 2)
-    _all_same((off, on, fast, sil))
+    off, on, fast, sil, auto = _frames(rt, s, "W9E1", BUNNY_CAM, 1920, 1080, (0, 0, 1920, 1080), 2)
+    _all_same((off, on, fast, sil, auto))
     # the point of it: far fewer nodes and triangles
     assert on[2]["node_interior"] < 0.75 * off[2]["node_interior"]
     assert fast[2]["node_interior"] < 0.6 * off[2]["node_interior"]

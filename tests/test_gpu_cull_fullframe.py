@@ -1,7 +1,7 @@
 """Subtree culling (RT_OPT_BSP_CULL, DESIGN.md section 4 "Subtree culling") on
 the BASELINE workloads at full size: every frame rendered with culling on --
-certified (the default, exact by proof), silhouette (round 5's opt-in camera
-bound, exact by proof) and fast (the round-3 margin, exact by these
+certified (the default, exact by proof), silhouette (round 5's camera bound,
+exact by proof), the timed choice between those two (auto) and fast (the round-3 margin, exact by these
 measurements only) -- equals the frame rendered with it off -- the reference's walk,
 bsp.wgsl:10-81, which the rest of the suite pins to the oracle and the oracle
 to the reference's own JS walk -- bit for bit: every pixel's accumulated
@@ -49,11 +49,12 @@ def test_full_frame_cull_equals_reference_walk(rt, gpu, configs, config, spp):
         ctx.set_uniforms(rt.make_uniform(*wl.camera, wl.width, wl.height))
         off = _frame(rt, ctx, wl, spp, rt._ffi.RT_BSP_CULL_OFF)
         ons = [_frame(rt, ctx, wl, spp, m) for m in (rt._ffi.RT_BSP_CULL_CERTIFIED, rt._ffi.RT_BSP_CULL_FAST,
-                                                      rt._ffi.RT_BSP_CULL_SILHOUETTE)]
+                                                      rt._ffi.RT_BSP_CULL_SILHOUETTE, rt._ffi.RT_BSP_CULL_AUTO)]
+        chosen = ctx.bsp_cull_in_use()
     finally:
         ctx.close()
     assert off[2]["subtree_culls"] == 0
-    for on, name in zip(ons, ("certified", "fast", "silhouette")):
+    for on, name in zip(ons, ("certified", "fast", "silhouette", "auto")):
         diff = int((off[0] != on[0]).any(axis=2).sum())
         assert diff == 0, f"config {config}: {diff} pixels' radiance differs with {name} culling"
         assert np.array_equal(off[1], on[1]), f"primary-hit ids differ with {name} culling"
@@ -65,4 +66,6 @@ def test_full_frame_cull_equals_reference_walk(rt, gpu, configs, config, spp):
               f"triangle tests {on[2]['tri_tests'] / off[2]['tri_tests']:.3f} of the unculled walk")
     # both modes really cull (the certified one too: a mode that culled nothing
     # would pass the equalities above trivially)
-    assert ons[0][2]["subtree_culls"] > 0 and ons[1][2]["subtree_culls"] > 0 and ons[2][2]["subtree_culls"] > 0
+    assert all(on[2]["subtree_culls"] > 0 for on in ons)
+    print(f"config {config}: RT_BSP_CULL_AUTO ran mode {chosen[0]} (probe: certified {chosen[1]:.2f} ms, "
+          f"silhouette {chosen[2]:.2f} ms)")

@@ -7,6 +7,7 @@
 #   ab<C>[f]:<v1>,<v2>,.. A/B of variants/<v>/lib02562rt.so on config C (2, 3, 4; 5 at 128 spp;
 #                         f: the fast margin)
 #   m<C>[fast] / m4sil    bench line + kernel-trace stats + PMC passes (tools/measure.sh)
+#   bench:a,b,..          one bench line (bench.py --no-cpu-baseline a b ..), no profiling
 #   n2 / n4 / n8          the same for rank 0's share of an N-rank split (bench.py --rank-share N)
 #   wf<C>[f] / wfpmc<C>   the wavefront split's price (tools/wavefront_price.py) / its PMC passes
 #   stress                tools/cull_stress.py: configs 3-5 whole frames, every culling mode
@@ -65,6 +66,14 @@ for step in "$@"; do
     m2) bash tools/measure.sh $TAG/c2 --config 2 --no-cpu-baseline || exit 1 ;;
     m4sil) bash tools/measure.sh $TAG/c4sil --config 4 --no-cpu-baseline --bsp-cull 3 || exit 1 ;;
     n2|n4|n8) bash tools/measure.sh $TAG/c3$step --no-cpu-baseline --rank-share ${step#n} || exit 1 ;;
+    m4auto) bash tools/measure.sh $TAG/c4auto --config 4 --no-cpu-baseline --bsp-cull 4 || exit 1 ;;
+    bench:*)
+      # one bench line, no profiling: bench:--config,4,--bsp-cull,4
+      a=$(echo ${step#bench:} | tr , ' ')
+      echo "== bench $a" >> $OUT/bench_lines.txt
+      timeout -k 10 600 python bench.py --no-cpu-baseline $a > $OUT/bench.tmp 2>&1 || { echo "bench rc=$?"; tail -20 $OUT/bench.tmp; exit 1; }
+      grep '^{' $OUT/bench.tmp >> $OUT/bench_lines.txt
+      grep '^{' $OUT/bench.tmp | python tools/bench_brief.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
