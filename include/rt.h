@@ -208,7 +208,8 @@ typedef struct rt_ray_counts {
 #define RT_BSP_CULL_AUTO       4  /* (default) exact as RT_BSP_CULL_CERTIFIED: the first W9E1 BSP render for a scene and eye
                                      times the certified and the silhouette kernels on a probe of itself (its first
                                      iterations, at most 2^25 samples, into the per-sample scratch only; accum and
-                                     ids untouched; two launches each) and runs the faster from then on, until the
+                                     ids untouched; two launches each) and runs the faster from then on (the
+                                     silhouette kernel must be 3 % faster to be chosen), until the
                                      BSP or the eye changes.  rt_bsp_cull_in_use reports the choice */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
