@@ -1,6 +1,6 @@
 """Subtree culling of the BSP walk (RT_OPT_BSP_CULL, rt_kernels.hip bsp_box_miss;
 DESIGN.md section 4 "Subtree culling") changes only the work, never the result:
-frames rendered with certified culling (the default; exact by proof), with the
+frames rendered with certified culling (exact by proof), with the
 silhouette bound and the timed choice between the two (RT_BSP_CULL_SILHOUETTE,
 RT_BSP_CULL_AUTO), with the fast margin (RT_BSP_CULL_FAST) and with culling off (every node of
 bsp.wgsl:10-81 visited) are equal bit for bit -- radiance, primary-hit ids and

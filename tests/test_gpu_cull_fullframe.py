@@ -1,6 +1,6 @@
 """Subtree culling (RT_OPT_BSP_CULL, DESIGN.md section 4 "Subtree culling") on
 the BASELINE workloads at full size: every frame rendered with culling on --
-certified (the default, exact by proof), silhouette (round 5's camera bound,
+certified (exact by proof), silhouette (round 5's camera bound,
 exact by proof), the timed choice between those two (auto) and fast (the round-3 margin, exact by these
 measurements only) -- equals the frame rendered with it off -- the reference's walk,
 bsp.wgsl:10-81, which the rest of the suite pins to the oracle and the oracle

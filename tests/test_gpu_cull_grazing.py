@@ -10,8 +10,9 @@ random distance (0.01 .. 1), so it grazes that triangle and crosses the cells
 around it; 30 % are any-hit walks (shadow rays).  Scenes: the config-5 style
 random soup (1M large, randomly oriented triangles) and the bunny stand-in.
 
-  * the default walk (RT_BSP_CULL_CERTIFIED), and the opt-in silhouette bound
-    (RT_BSP_CULL_SILHOUETTE, round 5), equal the CPU oracle's walk
+  * the certified walk (RT_BSP_CULL_CERTIFIED), and the silhouette bound
+    (RT_BSP_CULL_SILHOUETTE, round 5) -- the two kernels the default RT_BSP_CULL_AUTO
+    chooses between -- equal the CPU oracle's walk
     (bsp.wgsl:10-81, every node visited) ray for ray: triangle and distance
     bit for bit, hit or miss for the any-hit rays -- 0 differences -- and the
     unculled GPU walk in every field (triangle, distance, barycentrics);

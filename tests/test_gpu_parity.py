@@ -165,7 +165,7 @@ def test_shade_threshold_is_scheduling_only(rt, gpu, depth):
     # The shading threshold only schedules: every setting -- fixed 8, 16, 24 or 32,
     # lockstep (0 and 64), an explicit per-wave pair, and the default per-wave choice
     # from the wave's share of lanes inside a leaf (k_path; T_lo 16 / T_hi 32 with
-    # the default certified culling, 8 / 24 with the fast margin) -- renders the same
+    # the certified and auto culling, 8 / 24 with the fast margin) -- renders the same
     # bits.  Depth 9 makes a test-dominated walk (~300 triangles per leaf: the share
     # is high and the waves choose T_hi), depth 20 a walk-dominated one (T_lo).
     s = Scene(rt, rt.Mesh.synth_soup(150_000), "BSP", oracle_accel_from_product=True, bsp_depth=depth)

@@ -58,9 +58,9 @@ WHOLE_BUDGET = {
     # per-treelet precomputed form 108/93 and 64/56.
     # round 5: the zero-component slab of the cull (an infinite reciprocal, the
     # capped gap tolerance) and bsp_inv1's flag: 108/99 (W7E3 64/56 and 64/53 with
-    # the one-load hit resolve); the opt-in silhouette bound's instantiation 128/118.
+    # the one-load hit resolve); the silhouette bound's instantiation 128/118.
     "k_pathILi4ELi0ELb0ELi1": (108, 99),    # W9E1, BSP
-    "k_pathILi4ELi0ELb0ELi2": (128, 118),   # W9E1, BSP, RT_BSP_CULL_SILHOUETTE (opt-in)
+    "k_pathILi4ELi0ELb0ELi2": (128, 118),   # W9E1, BSP, RT_BSP_CULL_SILHOUETTE (auto picks it on config 4)
     "k_pathILi4ELi0ELb0ELi0": (88, 99),     # W9E1, BSP, the fast-margin instantiation
     "k_pathILi4ELi1ELb0ELi1": (80, 77),     # W9E1, BVH
     "k_pathILi3ELi0ELb0ELi1": (64, 56),     # W7E3, BSP at 7 waves/SIMD
