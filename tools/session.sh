@@ -67,6 +67,7 @@ for step in "$@"; do
     m4sil) bash tools/measure.sh $TAG/c4sil --config 4 --no-cpu-baseline --bsp-cull 3 || exit 1 ;;
     n2|n4|n8) bash tools/measure.sh $TAG/c3$step --no-cpu-baseline --rank-share ${step#n} || exit 1 ;;
     m4auto) bash tools/measure.sh $TAG/c4auto --config 4 --no-cpu-baseline --bsp-cull 4 || exit 1 ;;
+    m3bvh) bash tools/measure.sh $TAG/c3bvh --trav BVH --no-cpu-baseline || exit 1 ;;
     bench:*)
       # one bench line, no profiling: bench:--config,4,--bsp-cull,4
       a=$(echo ${step#bench:} | tr , ' ')
