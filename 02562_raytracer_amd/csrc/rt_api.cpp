@@ -1072,6 +1072,17 @@ int rt_trace_rays(rt_ctx* c, rt_traverse trav, const float* rays, const uint32_t
     return RT_OK;
 }
 
+// The shading threshold of a render (RT_OPT_SHADE_THRESHOLD, or the default per walk,
+// shader and the culling kernel `cull` that runs; render_common has the measurements).
+static uint32_t default_threshold(const rt_ctx* c, rt_mode mode, rt_traverse trav, uint32_t cull)
+{
+    if (c->shade_threshold >= 0) return (uint32_t)c->shade_threshold;
+    if (trav == RT_TRAVERSE_BVH) return 4u;
+    if (mode == RT_MODE_W7E3) return 24u;
+    if (cull == RT_BSP_CULL_SILHOUETTE) return (1u << 16) | (32u << 8) | 24u;
+    return cull_certified(c) ? (1u << 16) | (32u << 8) | 16u : (1u << 16) | (24u << 8) | 8u;
+}
+
 // RT_BSP_CULL_AUTO: times the certified and the silhouette W9E1 kernels on a probe of
 // the render about to run -- its first iterations over the whole region, at most 2^25
 // samples, written to the per-sample scratch only (no fold: accum and ids are
@@ -1079,8 +1090,9 @@ int rt_trace_rays(rt_ctx* c, rt_traverse trav, const float* rays, const uint32_t
 // Both are exact (the same frame bit for bit), so the choice moves only time: the
 // silhouette bound gains 15 % on config 4's far grid of bunnies and loses 3-4 % on
 // configs 3 and 5.  L: the render's launch with its scratch and
-// stride set; max_spp: the iterations that scratch holds.
-static int probe_auto_cull(rt_ctx* c, rtk::DevScene& S, const rtk::DevLaunch& L, uint32_t max_spp, rt_mode mode,
+// stride set (its shading threshold becomes the chosen kernel's); max_spp: the
+// iterations that scratch holds.
+static int probe_auto_cull(rt_ctx* c, rtk::DevScene& S, rtk::DevLaunch& L, uint32_t max_spp, rt_mode mode,
                            rt_traverse trav)
 {
     rtk::DevLaunch P = L;
@@ -1095,6 +1107,7 @@ static int probe_auto_cull(rt_ctx* c, rtk::DevScene& S, const rtk::DevLaunch& L,
                                RT_BSP_CULL_SILHOUETTE};
     for (int i = 0; i < 4; i++) {
         S.bsp_cull_mode = order[i];
+        P.shade_threshold = default_threshold(c, mode, trav, order[i]);   // (each kernel with its own)
         HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
         HIPCHK(c, hipEventRecord(c->auto_ev[2 * i], c->stream));
         const int r = rtk::launch_render(S, P, mode, trav, false, c->num_cus, c->waves_per_cu, c->stream);
@@ -1111,6 +1124,7 @@ static int probe_auto_cull(rt_ctx* c, rtk::DevScene& S, const rtk::DevLaunch& L,
     // kernel wins by 8 % (profiles/r05/ab_auto.txt)
     c->auto_cull = c->auto_ms[1] < 0.97f * c->auto_ms[0] ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
     S.bsp_cull_mode = cull_in_use(c);
+    L.shade_threshold = default_threshold(c, mode, trav, S.bsp_cull_mode);
     // the render's ray counts are its own: clear what the probe's launches counted
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
     return RT_OK;
@@ -1185,11 +1199,9 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // nodes and its rays take more trips, so finished lanes wait longer for the last
     // ones: 16 and 32 (profiles/r04/sweep_T.txt: config 3 fixed 16 +1.9 % over 8,
     // config 4 16..24 +3 %, config 5 32 +1.1 %).
-    const uint32_t adaptive = cull_certified(c) ? (1u << 16) | (32u << 8) | 16u : (1u << 16) | (24u << 8) | 8u;
-    L.shade_threshold = (uint32_t)(c->shade_threshold >= 0 ? c->shade_threshold
-                                   : trav == RT_TRAVERSE_BVH ? 4
-                                   : mode == RT_MODE_W7E3    ? 24
-                                                             : adaptive);
+    // The silhouette kernel's camera rays take fewer, dearer trips: 24 and 32
+    // (profiles/r05/sweep_T_c4s.txt: config 4 +1.2 % over 16 / 32).
+    L.shade_threshold = default_threshold(c, mode, trav, cull_in_use(c));
     L.reserved0 = 0;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));

@@ -11,7 +11,7 @@
 #   n2 / n4 / n8          the same for rank 0's share of an N-rank split (bench.py --rank-share N)
 #   wf<C>[f] / wfpmc<C>   the wavefront split's price (tools/wavefront_price.py) / its PMC passes
 #   stress                tools/cull_stress.py: configs 3-5 whole frames, every culling mode
-#   sweep<C>[f]:T1,..     shading-threshold sweep (tools/sweep_threshold.sh)
+#   sweep<C>[f|s]:T1,..   shading-threshold sweep (tools/sweep_threshold.sh; f fast, s silhouette)
 #   scale<C>              tools/scale_probe.py: each rank's share of the N-rank split, N = 1, 2, 4, 8
 set -u
 TAG=$1; shift
@@ -45,6 +45,7 @@ for step in "$@"; do
       # sweep<C>[f]:T1,T2,...  shading thresholds (tools/sweep_threshold.sh; -1 = the default)
       c=${step:5:1}; ts=$(echo ${step#*:} | tr , ' '); f=""; fo=""
       [ "${step:6:1}" = "f" ] && { f=f; fo="--bsp-cull 2"; }
+      [ "${step:6:1}" = "s" ] && { f=s; fo="--bsp-cull 3"; }
       case $c in 3) o="";; 4) o="--config 4";; 5) o="--config 5 --spp 128";; 2) o="--config 2";; esac
       bash tools/sweep_threshold.sh $OUT/sweep_c$c$f.txt "$o $fo" $ts || { tail -5 $OUT/sweep_c$c$f.txt; exit 1; }
       cat $OUT/sweep_c$c$f.txt ;;
