@@ -89,6 +89,22 @@ def test_auto_with_async_fold(rt):
     ctx.close()
 
 
+def test_cull_option_range(rt):
+    F = rt._ffi
+    ctx = rt.Context(0)
+    try:
+        assert ctx.bsp_cull_in_use() == (F.RT_BSP_CULL_CERTIFIED, 0.0, 0.0)   # the default auto, before a probe
+        for bad in (-1, F.RT_BSP_CULL_AUTO + 1):
+            with pytest.raises(Exception):
+                ctx.set_option(F.RT_OPT_BSP_CULL, bad)
+        ctx.set_option(F.RT_OPT_BSP_CULL, F.RT_BSP_CULL_FAST)
+        assert ctx.bsp_cull_in_use()[0] == F.RT_BSP_CULL_FAST
+        ctx.set_option(F.RT_OPT_BSP_CULL, F.RT_BSP_CULL_SILHOUETTE)
+        assert ctx.bsp_cull_in_use()[0] == F.RT_BSP_CULL_CERTIFIED   # no camera terms yet: the certified kernel
+    finally:
+        ctx.close()
+
+
 def test_auto_other_modes_do_not_probe(rt):
     F = rt._ffi
     s = Scene(rt, rt.Mesh.from_obj(model("CornellBoxWithBlocks.obj")), "BSP")
