@@ -11,6 +11,7 @@
 #   n2 / n4 / n8          the same for rank 0's share of an N-rank split (bench.py --rank-share N)
 #   wf<C>[f] / wfpmc<C>   the wavefront split's price (tools/wavefront_price.py) / its PMC passes
 #   stress                tools/cull_stress.py: configs 3-5 whole frames, every culling mode
+#   meshes                tools/mesh_frame.py: the config-3 frame on teapot.obj next to the stand-in
 #   sweep<C>[f|s]:T1,..   shading-threshold sweep (tools/sweep_threshold.sh; f fast, s silhouette)
 #   scale<C>              tools/scale_probe.py: each rank's share of the N-rank split, N = 1, 2, 4, 8
 set -u
@@ -69,6 +70,10 @@ for step in "$@"; do
     n2|n4|n8) bash tools/measure.sh $TAG/c3$step --no-cpu-baseline --rank-share ${step#n} || exit 1 ;;
     m4auto) bash tools/measure.sh $TAG/c4auto --config 4 --no-cpu-baseline --bsp-cull 4 || exit 1 ;;
     m3bvh) bash tools/measure.sh $TAG/c3bvh --trav BVH --no-cpu-baseline || exit 1 ;;
+    meshes)
+      # the headline frame's shape on the reference's teapot.obj next to the stand-in (tools/mesh_frame.py)
+      timeout -k 10 600 python tools/mesh_frame.py > $OUT/mesh_frame.json 2> $OUT/mesh_frame.err || { echo "mesh_frame rc=$?"; tail -20 $OUT/mesh_frame.err; exit 1; }
+      cat $OUT/mesh_frame.json ;;
     bench:*)
       # one bench line, no profiling: bench:--config,4,--bsp-cull,4
       a=$(echo ${step#bench:} | tr , ' ')
