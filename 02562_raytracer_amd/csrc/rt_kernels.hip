@@ -696,6 +696,14 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 #ifndef RT_AB_CULL_CAM
 #define RT_AB_CULL_CAM 1
 #endif
+// A/B probes only: the silhouette instantiation without its node-data load (zeros) or
+// without its arithmetic (the certified camera term)
+#ifndef RT_AB_SIL_NOLOAD
+#define RT_AB_SIL_NOLOAD 0
+#endif
+#ifndef RT_AB_SIL_NOMATH
+#define RT_AB_SIL_NOMATH 0
+#endif
 __device__ __forceinline__ float h2f(uint32_t bits) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits); }
 // CM 0: the fast margin's formula alone, m = max(|o|inf ko, dscene), for a
 // context whose culling is not certified (the host picks k_path's
@@ -747,7 +755,7 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
         const float winf = __builtin_fmaxf(__builtin_fmaxf(rt_absf(w.x), rt_absf(w.y)), rt_absf(w.z));
         const float dcam = __builtin_fmaf(winf, h2f(q5.x >> 16), 0.0f);   // G: f16 in the high half
         float dc = dcam;
-        if constexpr (CM == 2) {
+        if constexpr (CM == 2 && !RT_AB_SIL_NOMATH) {
             // RT_BSP_CULL_SILHOUETTE: the subtree's two triangles of smallest camera
             // term are bounded per ray by their own normals x = n*/E_t^2 (f16, q6; NaN
             // slots drop out of the minimum), the rest by G_x (q6.w): |denom| / E_t^2
@@ -888,7 +896,7 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
             const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
             off6 = (!in_leaf & cam) ? off6 : 0x80000000u;
         }
-        q6 = __builtin_amdgcn_raw_buffer_load_b128(rs6, off6, 0, 0);
+        if (!RT_AB_SIL_NOLOAD) q6 = __builtin_amdgcn_raw_buffer_load_b128(rs6, off6, 0, 0);
         asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6));
     } else {
         asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5));
