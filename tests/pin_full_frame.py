@@ -7,7 +7,7 @@ radiance word, the primary-hit id, the ray counts.  Config 4 (the 7M-triangle bu
 grid, 1920x1080 x 256 spp = 531 M samples) extends tests/test_gpu_configs.py's centre
 quarter to the whole frame.
 
-  python tests/pin_full_frame.py --config 4 [--spp N]
+  python tests/pin_full_frame.py --config 4 [--spp N] [--trav BVH]
 Prints one JSON line; exit status 1 if anything differs."""
 import argparse
 import importlib
@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--config", type=int, default=4)
     ap.add_argument("--spp", type=int, default=None)
     ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--trav", default=None, choices=["BSP", "BVH"], help="the walk (default: the workload's)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -37,7 +38,8 @@ def main():
     spp = a.spp or wl.spp
     W, H = wl.width, wl.height
     t0 = time.perf_counter()
-    s = Scene(rt, wl.mesh(), wl.traversal, env=wl.env, oracle_accel_from_product=True)
+    trav = a.trav or wl.traversal
+    s = Scene(rt, wl.mesh(), trav, env=wl.env, oracle_accel_from_product=True)
     t1 = time.perf_counter()
     g = s.render_gpu(wl.mode, wl.camera, W, H, (0, 0, W, H), 0, spp)
     used = s.ctx.bsp_cull_in_use()
@@ -62,8 +64,8 @@ def main():
     counts = {k: [int(g[2][k]), int(o[2][k])] for k in ("samples", "primary", "shadow", "bounce")}
     same = bits == 0 and idm == 0 and all(x == y for x, y in counts.values())
     print(json.dumps({
-        "config": a.config, "workload": f"{wl.name}, {W}x{H}, {spp} spp", "samples": W * H * spp,
-        "gpu_culling": {0: "off", 1: "certified", 2: "fast", 3: "silhouette"}[used[0]],
+        "config": a.config, "workload": f"{wl.name}, {W}x{H}, {spp} spp", "samples": W * H * spp, "traversal": trav,
+        "gpu_culling": {0: "off", 1: "certified", 2: "fast", 3: "silhouette"}[used[0]] if trav == "BSP" else None,
         "radiance_words_differing": int(bits), "primary_ids_differing": int(idm), "radiance_linf": linf,
         "ray_counts_gpu_oracle": counts, "equal": bool(same),
         "oracle_s": round(t3 - t2, 1), "oracle_threads": a.threads}), flush=True)
