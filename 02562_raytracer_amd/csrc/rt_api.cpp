@@ -1121,7 +1121,7 @@ static int probe_auto_cull(rt_ctx* c, rtk::DevScene& S, rtk::DevLaunch& L, uint3
     c->auto_ms[1] = std::min(t[1], t[3]);
     // the silhouette kernel must win by 3 %: on config 3 the two probe within 1-4 % of each
     // other (the certified kernel 4 % faster over whole frames), on config 4 the silhouette
-    // kernel wins by 8 % (profiles/r05/ab_auto.txt)
+    // kernel wins by 8-12 % (profiles/r05/ab_auto.txt, the final bench lines' bsp_cull)
     c->auto_cull = c->auto_ms[1] < 0.97f * c->auto_ms[0] ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
     S.bsp_cull_mode = cull_in_use(c);
     L.shade_threshold = default_threshold(c, mode, trav, S.bsp_cull_mode);
