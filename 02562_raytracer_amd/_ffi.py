@@ -132,7 +132,7 @@ SIGNATURES = {
     "rt_get_stream": (vp, [vp]),
     "rt_synchronize": (C.c_int, [vp]),
     "rt_set_option": (C.c_int, [vp, C.c_int, C.c_int64]),
-    "rt_bsp_cull_in_use": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_float)]),
+    "rt_bsp_cull_in_use": (C.c_int, [vp, C.POINTER(C.c_int), C.POINTER(C.c_float), C.POINTER(C.c_uint32)]),
     "rt_last_error": (C.c_char_p, [vp]),
     "rt_device_alloc": (C.c_int, [vp, C.c_size_t, C.POINTER(vp)]),
     "rt_device_free": (C.c_int, [vp, vp]),

@@ -266,8 +266,16 @@ class Context:
         kernels run now (rt_bsp_cull_in_use; RT_BSP_CULL_AUTO's choice once probed)."""
         m = C.c_int()
         ms = (C.c_float * 2)()
-        self._chk(F.lib().rt_bsp_cull_in_use(self._h, C.byref(m), ms))
+        self._chk(F.lib().rt_bsp_cull_in_use(self._h, C.byref(m), ms, None))
         return m.value, ms[0], ms[1]
+
+    def bsp_cull_probes(self):
+        """(probes started, probe launches) of RT_BSP_CULL_AUTO on this context
+        (rt_bsp_cull_in_use's probes)."""
+        m = C.c_int()
+        n = (C.c_uint32 * 2)()
+        self._chk(F.lib().rt_bsp_cull_in_use(self._h, C.byref(m), None, n))
+        return n[0], n[1]
 
     def upload_mesh(self, mesh):
         self._chk(F.lib().rt_upload_mesh_host(self._h, mesh.handle))

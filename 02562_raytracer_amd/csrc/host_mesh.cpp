@@ -16,6 +16,7 @@
 #include <sstream>
 #include <string>
 #include <unordered_map>
+#include <thread>
 #include <vector>
 
 #include "host_types.h"
@@ -454,44 +455,91 @@ extern "C" int rt_mesh_synth_bunny(uint32_t ntris_target, uint32_t seed, rt_mesh
 
 // 10M-style random triangle soup: centres U[-1,1]^3,
 // vertices = centre + U[-0.01,0.01]^3; 64-bit LCG (PCG32 output) seeded by `seed`.
+// Triangle t takes draws 12t .. 12t+11 of the one stream, so threads fill disjoint
+// triangle ranges from a jumped-ahead state (the same mesh, bit for bit, as one pass).
+static constexpr uint64_t SOUP_MUL = 6364136223846793005ull, SOUP_INC = 1442695040888963407ull;
+
+// the LCG state `delta` steps after `state` (Brown, "Random number generation with
+// arbitrary strides": the affine map's powers by squaring)
+static uint64_t lcg_advance(uint64_t state, uint64_t delta)
+{
+    uint64_t acc_mul = 1, acc_inc = 0, mul = SOUP_MUL, inc = SOUP_INC;
+    while (delta) {
+        if (delta & 1) {
+            acc_mul *= mul;
+            acc_inc = acc_inc * mul + inc;
+        }
+        inc = (mul + 1) * inc;
+        mul *= mul;
+        delta >>= 1;
+    }
+    return acc_mul * state + acc_inc;
+}
+
 extern "C" int rt_mesh_synth_soup(uint32_t ntris, uint32_t seed, rt_mesh_host** out)
 {
     if (!out || ntris == 0) {
         set_error("rt_mesh_synth_soup: bad argument");
         return RT_E_INVALID;
     }
-    uint64_t state = 0x853c49e6748fea9bull ^ ((uint64_t)seed << 1);
-    auto pcg = [&]() {
-        uint64_t old = state;
-        state = old * 6364136223846793005ull + 1442695040888963407ull;
-        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
-        uint32_t rot = (uint32_t)(old >> 59u);
-        return (xs >> rot) | (xs << ((-rot) & 31));
-    };
-    auto uni = [&](float lo, float hi) { return lo + (hi - lo) * (float)((pcg() >> 8) * (1.0 / 16777216.0)); };
+    const uint64_t state0 = 0x853c49e6748fea9bull ^ ((uint64_t)seed << 1);
     rt_mesh_host* m = new rt_mesh_host();
-    m->pos.reserve((size_t)ntris * 12);
-    m->idx.reserve((size_t)ntris * 4);
-    for (uint32_t t = 0; t < ntris; t++) {
-        float c[3] = {uni(-1, 1), uni(-1, 1), uni(-1, 1)};
-        for (int k = 0; k < 3; k++)
-            m->pos.insert(m->pos.end(), {c[0] + uni(-0.01f, 0.01f), c[1] + uni(-0.01f, 0.01f), c[2] + uni(-0.01f, 0.01f), 0.0f});
-        m->idx.insert(m->idx.end(), {3 * t, 3 * t + 1, 3 * t + 2, 0u});
-    }
-    m->nrm.assign(m->pos.size(), 0.0f);
-    for (uint32_t t = 0; t < ntris; t++) {   // face normal as vertex normal
-        float* p = &m->pos[(size_t)t * 12];
-        double e0[3], e1[3], n[3];
-        for (int c = 0; c < 3; c++) {
-            e0[c] = p[4 + c] - p[c];
-            e1[c] = p[8 + c] - p[c];
+    m->pos.resize((size_t)ntris * 12);
+    m->idx.resize((size_t)ntris * 4);
+    m->nrm.resize((size_t)ntris * 12);
+    auto fill = [&](uint32_t lo, uint32_t hi) {
+        uint64_t state = lcg_advance(state0, 12ull * lo);
+        auto pcg = [&]() {
+            uint64_t old = state;
+            state = old * SOUP_MUL + SOUP_INC;
+            uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+            uint32_t rot = (uint32_t)(old >> 59u);
+            return (xs >> rot) | (xs << ((-rot) & 31));
+        };
+        auto uni = [&](float a, float b) { return a + (b - a) * (float)((pcg() >> 8) * (1.0 / 16777216.0)); };
+        for (uint32_t t = lo; t < hi; t++) {
+            float* p = &m->pos[(size_t)t * 12];
+            const float c0 = uni(-1, 1), c1 = uni(-1, 1), c2 = uni(-1, 1);
+            for (int k = 0; k < 3; k++) {   // (the three offsets in argument order x, y, z)
+                const float ox = uni(-0.01f, 0.01f), oy = uni(-0.01f, 0.01f), oz = uni(-0.01f, 0.01f);
+                p[4 * k] = c0 + ox;
+                p[4 * k + 1] = c1 + oy;
+                p[4 * k + 2] = c2 + oz;
+                p[4 * k + 3] = 0.0f;
+            }
+            uint32_t* ix = &m->idx[(size_t)t * 4];
+            ix[0] = 3 * t;
+            ix[1] = 3 * t + 1;
+            ix[2] = 3 * t + 2;
+            ix[3] = 0u;
+            double e0[3], e1[3], n[3];   // face normal as vertex normal
+            for (int c = 0; c < 3; c++) {
+                e0[c] = p[4 + c] - p[c];
+                e1[c] = p[8 + c] - p[c];
+            }
+            n[0] = e0[1] * e1[2] - e0[2] * e1[1];
+            n[1] = e0[2] * e1[0] - e0[0] * e1[2];
+            n[2] = e0[0] * e1[1] - e0[1] * e1[0];
+            const double l = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
+            float* q = &m->nrm[(size_t)t * 12];
+            for (int k = 0; k < 3; k++) {
+                for (int c = 0; c < 3; c++) q[k * 4 + c] = l > 0 ? (float)(n[c] / l) : 0.0f;
+                q[k * 4 + 3] = 0.0f;
+            }
         }
-        n[0] = e0[1] * e1[2] - e0[2] * e1[1];
-        n[1] = e0[2] * e1[0] - e0[0] * e1[2];
-        n[2] = e0[0] * e1[1] - e0[1] * e1[0];
-        double l = sqrt(n[0] * n[0] + n[1] * n[1] + n[2] * n[2]);
-        for (int k = 0; k < 3; k++)
-            for (int c = 0; c < 3; c++) m->nrm[(size_t)t * 12 + k * 4 + c] = l > 0 ? (float)(n[c] / l) : 0.0f;
+    };
+    // (16 threads at most: the GPU box's per-GPU share of the host)
+    const uint32_t nthr = std::min<uint32_t>(std::max(1u, std::thread::hardware_concurrency()), 16);
+    if (ntris < 65536 || nthr == 1) {
+        fill(0, ntris);
+    } else {
+        std::vector<std::thread> th;
+        const uint32_t chunk = (ntris + nthr - 1) / nthr;
+        for (uint32_t k = 0; k < nthr; k++) {
+            const uint32_t lo = k * chunk, hi = std::min<uint32_t>(ntris, lo + chunk);
+            if (lo < hi) th.emplace_back(fill, lo, hi);
+        }
+        for (auto& t : th) t.join();
     }
     rt_material w;
     memset(&w, 0, sizeof w);

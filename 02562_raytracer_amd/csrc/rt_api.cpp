@@ -97,10 +97,18 @@ struct rt_ctx {
     float hcam_eye[3] = {0, 0, 0};
     DevBuf hcam_scratch;
     DevBuf bsp_sil;   // RT_BSP_CULL_SILHOUETTE's node data ((nnodes + 1) x 16 B)
-    // RT_BSP_CULL_AUTO: the certified form the W9E1 walk runs for this scene and eye
-    // (0: not probed yet; reset with the camera terms), and the probe's timings
+    // RT_BSP_CULL_AUTO (probe_plan / probe_finish): the exact kernel the W9E1 BSP walk
+    // runs for this scene (0: not decided yet), the probe's four timed launches --
+    // certified, silhouette, certified, silhouette, each one of the renders' own
+    // launches -- with their sample counts, the best time per 2^20 samples of each
+    // kernel, the eye reach the choice was made at (a reach outside [1/2, 2] of it
+    // probes again), and how many probes / probe launches this context has run
     uint32_t auto_cull = 0;
+    uint32_t probe_n = 0;
+    uint64_t probe_samples[4] = {0, 0, 0, 0};
     float auto_ms[2] = {0, 0};
+    float probe_reach = 0.0f;
+    uint32_t probes = 0, probe_launches = 0;
     hipEvent_t auto_ev[8] = {};
     DevBuf bvh_nodes, bvh_ids;   // bvh_nodes: [32-B nodes | 48-B records]
     DevBuf bvh_ref;              // the GpuNode array in the reference layout (rt_download_bvh)
@@ -358,6 +366,10 @@ int rt_set_option(rt_ctx* c, int option, int64_t value)
     case RT_OPT_BSP_CULL:
         if (value < RT_BSP_CULL_OFF || value > RT_BSP_CULL_AUTO)
             return fail(c, RT_E_INVALID, "BSP cull must be RT_BSP_CULL_OFF, _CERTIFIED, _FAST, _SILHOUETTE or _AUTO");
+        if (c->bsp_cull != (uint32_t)value) {   // (RT_BSP_CULL_AUTO starts over)
+            c->auto_cull = 0;
+            c->probe_n = 0;
+        }
         c->bsp_cull = (uint32_t)value;
         return RT_OK;
     case RT_OPT_UNIT_ORDER:
@@ -521,6 +533,8 @@ int rt_upload_mesh(rt_ctx* c, const float* pos_vec4, const float* nrm_vec4, uint
 static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off, size_t total, const float aabb[8])
 {
     c->hcam_valid = false;
+    c->auto_cull = 0;   // (a new scene: RT_BSP_CULL_AUTO probes again)
+    c->probe_n = 0;
     HIPCHK(c, c->bsp_nodes.alloc(total));
     DevBuf boxes;
     HIPCHK(c, boxes.alloc((size_t)nnodes * 64));
@@ -782,14 +796,25 @@ static bool cull_certified(const rt_ctx* c)
            c->bsp_cull == RT_BSP_CULL_AUTO;
 }
 
-// the mode the BSP kernels run: the silhouette bound needs its node data, made with the
-// camera terms (ensure_hcam), so without them (no uniforms, or a non-finite eye) it runs
-// the certified kernel; RT_BSP_CULL_AUTO runs its probe's choice (certified until probed)
-static uint32_t cull_in_use(const rt_ctx* c)
+// whether a render's walk has a silhouette instantiation: W9E1's BSP path kernel (not
+// its transparent form, selection1 7, launch_render); the query and batch kernels have
+// one too.  Every other kernel runs the certified form under SILHOUETTE and AUTO.
+static bool has_silhouette(const rt_ctx* c, rt_mode mode, rt_traverse trav)
 {
-    if (c->bsp_cull == RT_BSP_CULL_SILHOUETTE) return c->hcam_valid ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
-    if (c->bsp_cull == RT_BSP_CULL_AUTO)
-        return c->hcam_valid && c->auto_cull == RT_BSP_CULL_SILHOUETTE ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
+    return mode == RT_MODE_W9E1 && trav == RT_TRAVERSE_BSP && c->u.selection1 != 7u;
+}
+
+// the mode a BSP kernel runs (sil: it has a silhouette instantiation): the silhouette
+// bound needs its node data, made with the camera terms (ensure_hcam), so without them
+// (no uniforms, or a non-finite eye) it runs the certified kernel; RT_BSP_CULL_AUTO runs
+// its probe's choice (certified until the probe has decided)
+static uint32_t cull_in_use(const rt_ctx* c, bool sil = true)
+{
+    if (c->bsp_cull == RT_BSP_CULL_SILHOUETTE || c->bsp_cull == RT_BSP_CULL_AUTO) {
+        const bool s = sil && c->hcam_valid &&
+                       (c->bsp_cull == RT_BSP_CULL_SILHOUETTE || c->auto_cull == RT_BSP_CULL_SILHOUETTE);
+        return s ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
+    }
     return c->bsp_cull;
 }
 int rt_download_bsp_treelets(rt_ctx* c, void* dst, uint64_t cap_bytes, uint64_t* bytes)
@@ -805,7 +830,11 @@ int rt_download_bsp_treelets(rt_ctx* c, void* dst, uint64_t cap_bytes, uint64_t*
     if (int r = set_dev(c)) return r;   // (first: ensure_hcam may launch the camera-term kernels)
     if (int r = ensure_hcam(c)) return r;
     HIPCHK(c, hipMemcpyAsync(dst, c->bsp_nodes.p, nt, hipMemcpyDeviceToHost, c->stream));
-    if (c->bsp_sil.n >= ns) HIPCHK(c, hipMemcpyAsync(static_cast<uint8_t*>(dst) + nt, c->bsp_sil.p, ns,
+    // the silhouette section only when it was made for this BSP and the uniforms' eye
+    // (ensure_hcam leaves it alone in the uncertified modes)
+    const bool sil_now = c->hcam_valid && cull_certified(c) && c->has_u &&
+                         memcmp(c->u.camera_pos, c->hcam_eye, sizeof c->hcam_eye) == 0;
+    if (sil_now && c->bsp_sil.n >= ns) HIPCHK(c, hipMemcpyAsync(static_cast<uint8_t*>(dst) + nt, c->bsp_sil.p, ns,
                                                      hipMemcpyDeviceToHost, c->stream));
     else memset(static_cast<uint8_t*>(dst) + nt, 0, ns);
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -943,7 +972,6 @@ static int ensure_hcam(rt_ctx* c)
         return fail(c, RT_E_DEVICE, "BSP camera terms: launch failed");
     memcpy(c->hcam_eye, e, sizeof c->hcam_eye);
     c->hcam_valid = true;
-    c->auto_cull = 0;   // (RT_BSP_CULL_AUTO probes again for the new eye)
     return RT_OK;
 }
 
@@ -1083,62 +1111,119 @@ static uint32_t default_threshold(const rt_ctx* c, rt_mode mode, rt_traverse tra
     return cull_certified(c) ? (1u << 16) | (32u << 8) | 16u : (1u << 16) | (24u << 8) | 8u;
 }
 
-// RT_BSP_CULL_AUTO: times the certified and the silhouette W9E1 kernels on a probe of
-// the render about to run -- its first iterations over the whole region, at most 2^25
-// samples, written to the per-sample scratch only (no fold: accum and ids are
-// untouched) -- twice each, alternating, and keeps the faster for this scene and eye.
-// Both are exact (the same frame bit for bit), so the choice moves only time: the
+// RT_BSP_CULL_AUTO's probe.  The certified and the silhouette W9E1 kernels are both
+// exact (the same frame bit for bit), so the choice between them moves only time: the
 // silhouette bound gains 15 % on config 4's far grid of bunnies and loses 3-4 % on
-// configs 3 and 5.  L: the render's launch with its scratch and
-// stride set (its shading threshold becomes the chosen kernel's); max_spp: the
-// iterations that scratch holds.
-static int probe_auto_cull(rt_ctx* c, rtk::DevScene& S, rtk::DevLaunch& L, uint32_t max_spp, rt_mode mode,
-                           rt_traverse trav)
+// configs 3 and 5.  The probe costs no extra work: four of the
+// renders' own launches, each of at least 2^20 samples, run certified, silhouette,
+// certified, silhouette (a big render splits its first iterations into four such
+// launches, 1/16 of it each at most; 1-spp frames of at least 2^20 pixels give one
+// launch each, so a moving camera's frames finish the probe in four frames).  Their
+// events are read without waiting, at a later render (probe_finish): until then the
+// certified kernel runs.  The choice holds for the scene -- a new BSP, a change of the
+// culling option, or an eye whose reach (farthest distance to the scene box) leaves
+// [1/2, 2] of the reach it was made at starts a new probe; orbiting or small moves keep it.
+static constexpr uint64_t PROBE_MIN_SAMPLES = 1ull << 20;
+
+// the eye's farthest distance to the scene's box (|eye - centre| + half diagonal)
+static float eye_reach(const rt_ctx* c)
 {
-    rtk::DevLaunch P = L;
-    const uint64_t cap = std::max<uint64_t>(1, (1ull << 25) / std::max<uint32_t>(1, L.stride));
-    P.spp = (uint32_t)std::min<uint64_t>({(uint64_t)L.spp, (uint64_t)max_spp, cap});
-    P.chunk = 1;
-    P.nchunks = P.spp;
-    P.unit_order = c->unit_order;
-    for (hipEvent_t& e : c->auto_ev)
-        if (!e) HIPCHK(c, hipEventCreate(&e));
-    const uint32_t order[4] = {RT_BSP_CULL_CERTIFIED, RT_BSP_CULL_SILHOUETTE, RT_BSP_CULL_CERTIFIED,
-                               RT_BSP_CULL_SILHOUETTE};
-    for (int i = 0; i < 4; i++) {
-        S.bsp_cull_mode = order[i];
-        P.shade_threshold = default_threshold(c, mode, trav, order[i]);   // (each kernel with its own)
-        HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
-        HIPCHK(c, hipEventRecord(c->auto_ev[2 * i], c->stream));
-        const int r = rtk::launch_render(S, P, mode, trav, false, c->num_cus, c->waves_per_cu, c->stream);
-        if (r) return fail(c, r, std::string("culling probe launch failed: ") + hipGetErrorString(hipGetLastError()));
-        HIPCHK(c, hipEventRecord(c->auto_ev[2 * i + 1], c->stream));
+    double d2 = 0.0, h2 = 0.0;
+    for (int k = 0; k < 3; k++) {
+        const double ctr = 0.5 * ((double)c->aabb[k] + c->aabb[k + 3]);
+        const double half = 0.5 * ((double)c->aabb[k + 3] - c->aabb[k]);
+        d2 += ((double)c->u.camera_pos[k] - ctr) * ((double)c->u.camera_pos[k] - ctr);
+        h2 += half * half;
     }
-    HIPCHK(c, hipEventSynchronize(c->auto_ev[7]));
-    float t[4];
-    for (int i = 0; i < 4; i++) HIPCHK(c, hipEventElapsedTime(&t[i], c->auto_ev[2 * i], c->auto_ev[2 * i + 1]));
-    c->auto_ms[0] = std::min(t[0], t[2]);
-    c->auto_ms[1] = std::min(t[1], t[3]);
+    return (float)(std::sqrt(d2) + std::sqrt(h2));
+}
+
+// a finished probe's choice: read when its last event has completed (never waits)
+static int probe_finish(rt_ctx* c)
+{
+    if (c->auto_cull || c->probe_n < 4) return RT_OK;
+    const hipError_t q = hipEventQuery(c->auto_ev[7]);
+    if (q == hipErrorNotReady) return RT_OK;
+    HIPCHK(c, q);
+    float best[2] = {INFINITY, INFINITY};
+    for (int i = 0; i < 4; i++) {
+        float t;
+        HIPCHK(c, hipEventElapsedTime(&t, c->auto_ev[2 * i], c->auto_ev[2 * i + 1]));
+        best[i & 1] = std::min(best[i & 1], (float)(t * (double)PROBE_MIN_SAMPLES / (double)c->probe_samples[i]));
+    }
+    c->auto_ms[0] = best[0];
+    c->auto_ms[1] = best[1];
     // the silhouette kernel must win by 3 %: on config 3 the two probe within 1-4 % of each
     // other (the certified kernel 4 % faster over whole frames), on config 4 the silhouette
     // kernel wins by 8-12 % (profiles/r05/ab_auto.txt, the final bench lines' bsp_cull)
-    c->auto_cull = c->auto_ms[1] < 0.97f * c->auto_ms[0] ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
-    S.bsp_cull_mode = cull_in_use(c);
-    L.shade_threshold = default_threshold(c, mode, trav, S.bsp_cull_mode);
-    // the render's ray counts are its own: clear what the probe's launches counted
-    HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
+    c->auto_cull = best[1] < 0.97f * best[0] ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
     return RT_OK;
 }
 
-int rt_bsp_cull_in_use(rt_ctx* c, int* mode, float* probe_ms)
+// the probe's part of a W9E1 BSP render under RT_BSP_CULL_AUTO, before its launches:
+// finish a completed probe, and start over when the eye's reach moved out of range
+static int probe_begin(rt_ctx* c)
+{
+    if (int r = probe_finish(c)) return r;
+    if (c->auto_cull || c->probe_n) {
+        const float reach = eye_reach(c);
+        if (!(reach <= 2.0f * c->probe_reach && reach >= 0.5f * c->probe_reach)) {
+            c->auto_cull = 0;
+            c->probe_n = 0;
+        }
+    }
+    return RT_OK;
+}
+
+// how many of a launch's n iterations (stride samples each, total in the whole render)
+// become the probe's next timed launch, 0 for none
+static uint32_t probe_take(const rt_ctx* c, uint32_t n, uint32_t total, uint32_t stride)
+{
+    if (c->auto_cull || c->probe_n >= 4 || stride == 0) return 0;
+    const uint64_t need = (PROBE_MIN_SAMPLES + stride - 1) / stride;
+    if (n < need) return 0;
+    const uint64_t cap = std::max<uint64_t>(1, (1ull << 25) / stride);
+    const uint64_t want = std::max<uint64_t>(need, std::min<uint64_t>(total / 16, cap));
+    return (uint32_t)std::min<uint64_t>(n, want);
+}
+
+int rt_bsp_cull_in_use(rt_ctx* c, int* mode, float* probe_ms, uint32_t* probes)
 {
     if (!c || !mode) return RT_E_INVALID;
+    if (c->bsp_cull == RT_BSP_CULL_AUTO && c->probe_n == 4 && !c->auto_cull) {
+        if (int r = set_dev(c)) return r;
+        if (int r = probe_finish(c)) return r;
+    }
     *mode = (int)cull_in_use(c);
     if (probe_ms) {
         const bool probed = c->bsp_cull == RT_BSP_CULL_AUTO && c->auto_cull != 0;
         probe_ms[0] = probed ? c->auto_ms[0] : 0.0f;
         probe_ms[1] = probed ? c->auto_ms[1] : 0.0f;
     }
+    if (probes) {
+        probes[0] = c->probes;
+        probes[1] = c->probe_launches;
+    }
+    return RT_OK;
+}
+
+// a render launch; slot >= 0: the probe's launch `slot`, bracketed by its events
+static int probe_launch(rt_ctx* c, const rtk::DevScene& S, const rtk::DevLaunch& L, rt_mode mode, rt_traverse trav,
+                        int slot)
+{
+    if (slot < 0) return launch_timed(c, S, L, mode, trav);
+    for (hipEvent_t& e : c->auto_ev)
+        if (!e) HIPCHK(c, hipEventCreate(&e));
+    if (slot == 0) {
+        c->probes++;
+        c->probe_reach = eye_reach(c);
+    }
+    HIPCHK(c, hipEventRecord(c->auto_ev[2 * slot], c->stream));
+    if (int r = launch_timed(c, S, L, mode, trav)) return r;
+    HIPCHK(c, hipEventRecord(c->auto_ev[2 * slot + 1], c->stream));
+    c->probe_samples[slot] = (uint64_t)L.stride * L.spp;
+    c->probe_n = (uint32_t)slot + 1;
+    c->probe_launches++;
     return RT_OK;
 }
 
@@ -1201,7 +1286,9 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // config 4 16..24 +3 %, config 5 32 +1.1 %).
     // The silhouette kernel's camera rays take fewer, dearer trips: 24 and 32
     // (profiles/r05/sweep_T_c4s.txt: config 4 +1.2 % over 16 / 32).
-    L.shade_threshold = default_threshold(c, mode, trav, cull_in_use(c));
+    const bool sil = has_silhouette(c, mode, trav);
+    S.bsp_cull_mode = cull_in_use(c, sil);
+    L.shade_threshold = default_threshold(c, mode, trav, S.bsp_cull_mode);
     L.reserved0 = 0;
     L.counters = c->counters.as<unsigned long long>();
     HIPCHK(c, hipMemsetAsync(c->counters.p, 0, 32 * sizeof(unsigned long long), c->stream));
@@ -1221,19 +1308,28 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
         if (c->samples.n < need) HIPCHK(c, c->samples.alloc(need));
         if (async && c->samples2.n < need) HIPCHK(c, c->samples2.alloc(need));
         L.samples = c->samples.as<float4>();
-        if (mode == RT_MODE_W9E1 && trav == RT_TRAVERSE_BSP && c->bsp_cull == RT_BSP_CULL_AUTO && c->hcam_valid &&
-            c->auto_cull == 0) {
-            if (int r = set_dev(c)) return r;   // (a pending fold may still read the scratch)
-            if (int r = probe_auto_cull(c, S, L, pass_spp, mode, trav)) return r;
-        }
+        const bool autop = sil && c->bsp_cull == RT_BSP_CULL_AUTO && c->hcam_valid;
+        if (autop)
+            if (int r = probe_begin(c)) return r;
         if (async) {   // the folds follow the context stream's work up to here
             HIPCHK(c, hipEventRecord(c->ev_enter, c->stream));
             HIPCHK(c, hipStreamWaitEvent(c->fold_stream, c->ev_enter, 0));
         }
         const uint32_t first = L.first_iter, total = L.spp;
-        for (uint32_t done = 0; done < total; done += pass_spp) {
+        for (uint32_t done = 0; done < total; done += L.spp) {
             L.first_iter = first + done;
             L.spp = std::min(pass_spp, total - done);
+            // RT_BSP_CULL_AUTO: this launch may be one of the probe's four (probe_take)
+            const uint32_t take = autop ? probe_take(c, L.spp, total, L.stride) : 0;
+            int slot = -1;
+            if (take) {
+                slot = (int)c->probe_n;
+                L.spp = take;
+                S.bsp_cull_mode = (slot & 1) ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
+            } else {
+                S.bsp_cull_mode = cull_in_use(c, sil);
+            }
+            L.shade_threshold = default_threshold(c, mode, trav, S.bsp_cull_mode);
             // work units (chunk, pixel slot) must stay below 2^31: widen chunks if needed
             uint32_t ch = std::max<uint32_t>(1, std::min(c->sample_chunk, L.spp));
             while ((uint64_t)L.nwork * 64u * ((L.spp + ch - 1) / ch) >= (1ull << 31)) ch *= 2;
@@ -1246,7 +1342,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
                 L.samples = (b ? c->samples2 : c->samples).as<float4>();
                 HIPCHK(c, hipStreamWaitEvent(c->stream, c->ev_free[b], 0));
                 HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
-                if (int r = launch_timed(c, S, L, mode, trav)) return r;
+                if (int r = probe_launch(c, S, L, mode, trav, slot)) return r;
                 HIPCHK(c, hipEventRecord(c->ev_path, c->stream));
                 HIPCHK(c, hipStreamWaitEvent(c->fold_stream, c->ev_path, 0));
                 const int r = rtk::launch_fold(L, c->fold_stream);
@@ -1256,7 +1352,7 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
                 continue;
             }
             HIPCHK(c, hipMemsetAsync(c->work.p, 0, 4096, c->stream));
-            if (int r = launch_timed(c, S, L, mode, trav)) return r;
+            if (int r = probe_launch(c, S, L, mode, trav, slot)) return r;
             const int r = rtk::launch_fold(L, c->stream);
             if (r) return fail(c, r, std::string("fold launch failed: ") + hipGetErrorString(hipGetLastError()));
         }

@@ -176,6 +176,21 @@ def roofline(key, kern_ms, alg_bytes, config, kernel):
     return r
 
 
+class DeviceAccel:
+    """The context's device-built BSP / HLBVH, downloaded on demand (the CPU
+    baseline's oracle renders from the same arrays), with BspTree's / Bvh's
+    arrays() shape."""
+
+    def __init__(self, ctx, trav):
+        self.ctx, self.trav = ctx, trav
+
+    def arrays(self):
+        if self.trav == "BSP":
+            tree, planes, ids, aabb = self.ctx.download_bsp()
+            return tree, planes, ids, aabb, 20
+        return self.ctx.download_bvh()
+
+
 def all_reduce(dist, t, op):
     """In place on the device under RCCL; through host memory under gloo."""
     if dist.get_backend() == "nccl":
@@ -213,6 +228,10 @@ def main():
     ap.add_argument("--waves-per-cu", type=int, default=None)
     ap.add_argument("--sample-chunk", type=int, default=None)
     ap.add_argument("--unit-order", type=int, default=None)
+    ap.add_argument("--host-build", action="store_true",
+                    help="build the BSP / HLBVH on the host (rt_bsp_build / rt_bvh_build) instead of on the "
+                         "device (rt_build_bsp_device / rt_build_bvh_device: the same arrays bit for bit, "
+                         "tests/test_gpu_bsp_build.py, test_gpu_build.py; 27 ms against 3.3 s for config 5)")
     ap.add_argument("--bsp-cull", type=int, default=None,
                     help="RT_OPT_BSP_CULL: 0 off, 1 certified, 2 fast margin, 3 certified + silhouette bound, "
                          "4 the faster of 1 and 3 by a timed probe (the library default)")
@@ -288,15 +307,21 @@ def main():
         ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, args.bsp_cull)
     if args.async_fold:
         ctx.set_option(rt._ffi.RT_OPT_ASYNC_FOLD, 1)
+    t_mesh = time.perf_counter() - t0
     ctx.upload_mesh(mesh)
-    if trav == "BSP":
-        accel = mesh.bsp_tree()
-        ctx.upload_bsp(accel)
+    # every rank builds its own replica of the scene's acceleration structure on its
+    # GPU (replicas per GPU): no host build per rank on a shared host
+    t1 = time.perf_counter()
+    if args.host_build:
+        accel = mesh.bsp_tree() if trav == "BSP" else mesh.bvh()
+        ctx.upload_bsp(accel) if trav == "BSP" else ctx.upload_bvh(accel)
     else:
-        accel = mesh.bvh()
-        ctx.upload_bvh(accel)
+        accel = DeviceAccel(ctx, trav)
+        ctx.build_bsp_device(20, 4) if trav == "BSP" else ctx.build_bvh_device(4)
     ctx.set_environment(wl.env)
     ctx.set_uniforms(rt.make_uniform(*cam, W, H, selection1=0))
+    torch.cuda.synchronize(dev)
+    t_accel = time.perf_counter() - t1
     setup_s = time.perf_counter() - t0
 
     lt = rt.local_tiles(W, H, nsplit)
@@ -408,10 +433,17 @@ def main():
     # per-rank step breakdown (ms per step): k_path, the gather's transfers, the unpack
     mine = torch.tensor([kern_total / args.steps, xfer_total / args.steps, unpack_total / args.steps],
                         dtype=torch.float64, device=dev)
+    # every rank's culling kernel (RT_BSP_CULL_*; each rank probes its own share) and probes
+    cull_mine = ctx.bsp_cull_in_use()
+    probes_mine = ctx.bsp_cull_probes()
+    cm = torch.tensor([cull_mine[0], cull_mine[1], cull_mine[2], probes_mine[0], probes_mine[1]],
+                      dtype=torch.float64, device=dev)
     if use_dist:
         per_rank = all_gather(dist, mine, world)
+        cull_ranks = all_gather(dist, cm, world)
     else:
         per_rank = mine.cpu().numpy()[None, :]
+        cull_ranks = cm.cpu().numpy()[None, :]
 
     value = rays[0] * args.steps / elapsed / 1e6
     if rank == 0:
@@ -422,13 +454,13 @@ def main():
         # the culling mode the kernel ran (RT_BSP_CULL_AUTO: its probe's choice, made in
         # the first warm-up step) picks the instantiation and the PMC summary
         names = {0: "off", 1: "certified", 2: "fast", 3: "silhouette"}
-        if hasattr(rt._ffi.lib(), "rt_bsp_cull_in_use"):
-            cull, probe_c, probe_s = ctx.bsp_cull_in_use()
-        else:   # (an A/B variant of an earlier tree)
-            cull, probe_c, probe_s = args.bsp_cull if args.bsp_cull is not None else rt._ffi.RT_BSP_CULL_CERTIFIED, 0, 0
+        cull, probe_c, probe_s = cull_mine
         cull_name = names[cull] if trav == "BSP" else None
         if trav == "BSP" and probe_c > 0:
-            cull_name = f"auto: {cull_name} (probe: certified {probe_c:.2f} ms, silhouette {probe_s:.2f} ms)"
+            cull_name = (f"auto: {cull_name} (probe: certified {probe_c:.3f}, silhouette {probe_s:.3f} ms per "
+                         f"2^20 samples)")
+        cull_per_rank = [names[int(r[0])] for r in cull_ranks] if trav == "BSP" else None
+        probes_per_rank = [[int(r[3]), int(r[4])] for r in cull_ranks] if trav == "BSP" else None
         roof = roofline(pmc_key(W, H, spp, trav, nsplit, args.config, cull), kern_ms_own, bytes_per_launch, args.config,
                         f"k_path<{wl.mode},{trav}>")
         roof["launches_per_step"] = launches_per_step
@@ -447,6 +479,11 @@ def main():
                        "parallelism": f"tiles8x8/{nsplit}",
                        # RT_OPT_BSP_CULL: the subtree culling (a different k_path instantiation per mode)
                        "bsp_cull": cull_name,
+                       # every rank's kernel and its probes (started, launches): each rank
+                       # decides on its own share of the frame
+                       "bsp_cull_per_rank": cull_per_rank,
+                       "bsp_cull_probes_per_rank": probes_per_rank,
+                       "accel_build": "host" if args.host_build else "device",
                        "world_size": dist.get_world_size() if use_dist else 1,
                        "backend": dist.get_backend() if use_dist else None,
                        "fold": "async (RT_OPT_ASYNC_FOLD)" if args.async_fold else "sync",
@@ -478,6 +515,9 @@ def main():
                                                             "memwait_cycles", "subtree_culls")},
             "simd_lane_util": round(detail["lane_steps"] / max(1, 64 * detail["trips"]), 4),
             "setup_s": round(setup_s, 3),
+            # setup_s split: the synthetic mesh (generated on the host), the acceleration
+            # structure's build + the uniforms (on the device unless --host-build)
+            "setup_breakdown_s": {"mesh": round(t_mesh, 3), "accel": round(t_accel, 3)},
         }
         print(json.dumps(line), flush=True)
         if args.dump_frame:

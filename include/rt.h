@@ -205,12 +205,15 @@ typedef struct rt_ray_counts {
                                      their camera term.  Fewer trips for far, many-object views (config 4: +15 %),
                                      more arithmetic per trip (config 3: -4 %, config 5: -3 %).  The W9E1
                                      path kernel and rt_trace_batch use it; other kernels run the certified form */
-#define RT_BSP_CULL_AUTO       4  /* (default) exact as RT_BSP_CULL_CERTIFIED: the first W9E1 BSP render for a scene and eye
-                                     times the certified and the silhouette kernels on a probe of itself (its first
-                                     iterations, at most 2^25 samples, into the per-sample scratch only; accum and
-                                     ids untouched; two launches each) and runs the faster from then on (the
-                                     silhouette kernel must be 3 % faster to be chosen), until the
-                                     BSP or the eye changes.  rt_bsp_cull_in_use reports the choice */
+#define RT_BSP_CULL_AUTO       4  /* (default) exact as RT_BSP_CULL_CERTIFIED: the W9E1 BSP renders time the
+                                     certified and the silhouette kernels on four of their own launches (certified,
+                                     silhouette, certified, silhouette; each at least 2^20 samples: a big render
+                                     splits its first iterations, 1-spp frames give one launch each), with no extra
+                                     work and no host wait (the events are read at a later render; the certified
+                                     kernel runs until then), and run the faster from then on (the silhouette
+                                     kernel must be 3 % faster to be chosen), until the BSP or this option changes
+                                     or the eye's reach (farthest distance to the scene box) leaves [1/2, 2] of the
+                                     reach the probe ran at.  rt_bsp_cull_in_use reports the choice */
 
 /* ---- device / context (replaces src/gpu_handles.rs) -------------------- */
 
@@ -232,12 +235,15 @@ int rt_synchronize(rt_ctx* ctx);
 
 int rt_set_option(rt_ctx* ctx, int option, int64_t value);
 
-/* The culling mode the BSP kernels run now (RT_BSP_CULL_*): the option's value, except
- * that RT_BSP_CULL_SILHOUETTE without the eye's camera terms runs CERTIFIED and
- * RT_BSP_CULL_AUTO runs its probe's choice (CERTIFIED or SILHOUETTE; CERTIFIED until
- * the probe has run for the current BSP and eye).  probe_ms (2 floats, or NULL): the
- * probe's best certified and silhouette launch times, 0 when it has not run. */
-int rt_bsp_cull_in_use(rt_ctx* ctx, int* mode, float* probe_ms);
+/* The culling mode the W9E1 BSP path kernel (and the query and batch kernels) run now
+ * (RT_BSP_CULL_*): the option's value, except that RT_BSP_CULL_SILHOUETTE without the
+ * eye's camera terms runs CERTIFIED and RT_BSP_CULL_AUTO runs its probe's choice
+ * (CERTIFIED or SILHOUETTE; CERTIFIED until a probe has decided for the current BSP).
+ * Kernels without a silhouette form (the other modes, W9E1's transparent shader) run
+ * CERTIFIED under SILHOUETTE and AUTO.  probe_ms (2 floats, or NULL): the probe's best
+ * certified and silhouette times in milliseconds per 2^20 samples, 0 until it has decided.
+ * probes (2 uint32, or NULL): the probes this context has started and their launches. */
+int rt_bsp_cull_in_use(rt_ctx* ctx, int* mode, float* probe_ms, uint32_t* probes);
 
 /* Message describing the last failure on this context (or the last
  * context-less failure when ctx == NULL).  Never NULL. */

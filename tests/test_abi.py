@@ -55,7 +55,7 @@ def test_error_codes_without_gpu(rt):
     assert L.rt_tileset_local_tiles(70, 45, 3) == (9 * 6 + 2) // 3
     assert L.rt_tileset_local_tiles(16, 16, 0) == 0
     m = C.c_int(-1)
-    assert L.rt_bsp_cull_in_use(None, C.byref(m), None) == rt._ffi.RT_E_INVALID
+    assert L.rt_bsp_cull_in_use(None, C.byref(m), None, None) == rt._ffi.RT_E_INVALID
 
 
 def test_scene_table_mirrors_reference(rt):

@@ -69,6 +69,12 @@ def test_two_rank_bench_frame_equals_one_rank(tmp_path, rt, oracle):
     _check_breakdown(two, 2)
     assert two["step_breakdown"]["gather_timer"].startswith("host wall time")
     assert one["config"]["bsp_cull"] == "certified"
+    # every rank's culling kernel and probes in the line (W7E3 has no silhouette form:
+    # certified, no probe), and the ranks' BSPs built on the device
+    assert one["config"]["bsp_cull_per_rank"] == ["certified"]
+    assert two["config"]["bsp_cull_per_rank"] == ["certified"] * 2
+    assert two["config"]["bsp_cull_probes_per_rank"] == [[0, 0]] * 2
+    assert two["config"]["accel_build"] == "device"
     assert two["n_gpus"] == 2 and two["config"]["world_size"] == 2 and two["config"]["backend"] == "gloo"
     assert one["config"]["world_size"] == 1
     # every ray counted once across the ranks
@@ -90,6 +96,8 @@ def test_eight_rank_bench_frame_equals_one_rank(tmp_path):
     one, f1 = _bench(1, str(tmp_path / "n1.npz"))
     eight, f8 = _bench(8, str(tmp_path / "n8.npz"))
     assert eight["n_gpus"] == 8 and eight["config"]["world_size"] == 8
+    assert eight["config"]["bsp_cull_per_rank"] == ["certified"] * 8
+    assert len(eight["config"]["bsp_cull_probes_per_rank"]) == 8
     _check_breakdown(eight, 8)
     assert eight["rays_per_step"] == one["rays_per_step"]
     assert np.array_equal(f1["ids"], f8["ids"])
@@ -132,3 +140,25 @@ def test_rank_share_renders_rank0_tiles(tmp_path):
     # 25 x 17 = 425 whole tiles (200 and 136 are multiples of 8); rank 0 of 4
     # holds tiles 0, 4, ..., 424: 107 tiles, one primary ray per pixel-iteration
     assert line["rays_per_step"]["primary"] == 107 * 64 * SPP
+
+
+def test_config5_setup_under_a_second_and_per_rank_cull(tmp_path):
+    """config 5's 10M-triangle BSP is built on the device
+    (rt_build_bsp_device; the host build took 3.3 s per rank), and the W9E1 line
+    reports each rank's auto-culling choice.  Two ranks over gloo on the one GPU,
+    a small frame of the real config-5 scene."""
+    env = dict(os.environ, RT_BENCH_DEVICE="0", RT_BENCH_DIST_BACKEND="gloo", OMP_NUM_THREADS="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "2",
+           "--config", "5", "--spp", "16", "--width", "1920", "--height", "1080", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][0])
+    print(json.dumps({k: line[k] for k in ("setup_s", "setup_breakdown_s", "value")}),
+          line["config"]["bsp_cull_per_rank"], line["config"]["bsp_cull_probes_per_rank"])
+    assert line["config"]["accel_build"] == "device"
+    assert line["setup_breakdown_s"]["accel"] < 1.0
+    assert len(line["config"]["bsp_cull_per_rank"]) == 2
+    assert all(c in ("certified", "silhouette") for c in line["config"]["bsp_cull_per_rank"])
+    # each rank probed once (the first step's four launches) and decided by the timed step
+    assert line["config"]["bsp_cull_probes_per_rank"] == [[1, 4], [1, 4]]

@@ -70,6 +70,8 @@ for step in "$@"; do
     n2|n4|n8) bash tools/measure.sh $TAG/c3$step --no-cpu-baseline --rank-share ${step#n} || exit 1 ;;
     m4auto) bash tools/measure.sh $TAG/c4auto --config 4 --no-cpu-baseline --bsp-cull 4 || exit 1 ;;
     m3bvh) bash tools/measure.sh $TAG/c3bvh --trav BVH --no-cpu-baseline || exit 1 ;;
+    m4bvh) bash tools/measure.sh $TAG/c4bvh --config 4 --trav BVH --no-cpu-baseline || exit 1 ;;
+    m5bvh) bash tools/measure.sh $TAG/c5bvh --config 5 --trav BVH --no-cpu-baseline ${M5BVH_OPTS:-} || exit 1 ;;
     meshes)
       # the headline frame's shape on the reference's teapot.obj next to the stand-in (tools/mesh_frame.py)
       timeout -k 10 600 python tools/mesh_frame.py > $OUT/mesh_frame.json 2> $OUT/mesh_frame.err || { echo "mesh_frame rc=$?"; tail -20 $OUT/mesh_frame.err; exit 1; }

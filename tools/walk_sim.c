@@ -75,6 +75,17 @@ int g_axis = 1;
 void walk_sim_axis(int a) { g_axis = a; }   /* nnodes x 6: content box (min.xyz, max.xyz) of each node's subtree, or NULL */
 void walk_sim_boxes(const float* b) { g_boxes = b; }
 static float g_tn, g_tf;   /* the ray interval clipped to the last tested box */
+/* WALK_SPEC: the speculative exact cull.  The walk culls when the
+ * certified margin proves it *or* the fast margin (2^-10 of max(|o|inf, scene)) culls,
+ * and decides against the intersection of the two clipped intervals; a ray is flagged
+ * when a cull or a near-/far-only decision rested on the fast margin alone (the
+ * certified test would not have made it).  An unflagged ray's walk made only proven
+ * decisions (its hit is the reference's); a flagged ray is re-walked certified. */
+int g_spec = 0, g_spec_flag = 0;
+static float g_tn_c = -INFINITY, g_tf_c = INFINITY;   /* the certified interval of the last box test */
+void walk_sim_spec(int sp) { g_spec = sp; }
+double g_spec_stat[8];   /* flagged rays, spec-only culls, spec-only clip decisions, proven culls, rewalk trips */
+void walk_sim_spec_stats(double* o) { for (int i = 0; i < 8; i++) o[i] = g_spec_stat[i]; }
 /* WALK_CERT: the certified margin (DESIGN.md section 4 "Certified culling"):
  * g_cert[node*7] = E2 (max over the subtree's triangles of max(|e0|inf, |e1|inf)^2),
  * +1..3 / +4..6 = the box of n* / (2 E2) over them (lower / upper) */
@@ -292,6 +303,29 @@ static int box_miss(uint32_t node, v3 o, v3 d, float tmin, float tmax)
                 g_camx_stat[2] += 1;
             }
         }
+        if (g_spec) {
+            /* the fast margin's cull and interval beside the certified ones */
+            double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));
+            double mf = fmax(om, g_cert_mag) * 0x1p-10;
+            double a0 = tmin, a1 = tmax;
+            int fmiss = 0;
+            for (int k = 0; k < 3; k++) {
+                double dk = comp(d, k), ok = comp(o, k);
+                if (fabs(dk) < 1e-8) { if (g_axis && dk == 0.0f && (ok < b[k] - mf || ok > b[3 + k] + mf)) fmiss = 1; continue; }
+                double a = (b[k] - mf - ok) / dk, cc = (b[3 + k] + mf - ok) / dk;
+                if (a > cc) { double x = a; a = cc; cc = x; }
+                if (a > a0) a0 = a;
+                if (cc < a1) a1 = cc;
+            }
+            fmiss = fmiss || a0 > a1 + (fabs(a0) + fabs(a1)) * 0x1p-18;
+            g_tn_c = (float)t0;
+            g_tf_c = (float)t1;
+            if (miss) { g_spec_stat[3] += 1; return 1; }
+            if (fmiss) { g_spec_stat[1] += 1; g_spec_flag = 1; return 1; }
+            g_tn = (float)(a0 > t0 ? a0 : t0);
+            g_tf = (float)(a1 < t1 ? a1 : t1);
+            return 0;
+        }
         if (!miss) {
             /* would the fast margin (2^-10 of max(|o|, scene)) have culled? */
             double om = fmax(fmax(fabs(o.x), fabs(o.y)), fabs(o.z));
@@ -460,8 +494,10 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
             float den = fabsf(ad) < 1.0e-8f ? 1.0e-8f : ad;
             float t = (s->planes[node] - ao) / den;
             if (t > tmax || t > ctf) {
+                if (g_spec && !(t > tmax) && !(t > g_tf_c)) { g_spec_flag = 1; g_spec_stat[2] += 1; }
                 node = nearn;
             } else if (t < tmin || t < ctn) {
+                if (g_spec && !(t < tmin) && !(t < g_tn_c)) { g_spec_flag = 1; g_spec_stat[2] += 1; }
                 node = farn;
             } else if ((var == 1 || var == 2 || var == 3) && is_empty_leaf(s, nearn)) {
                 /* push + visit the empty near leaf + pop, folded: the counted
@@ -516,7 +552,23 @@ int walk_sim(const uint32_t* tree, const float* planes, const uint32_t* ids, con
         for (int v = 1; v < (g_boxes ? 5 : 3); v++) {
             hv = -1;
             tv = ~0u;
+            g_spec_flag = 0;
+            g_tn_c = -INFINITY;
+            g_tf_c = INFINITY;
             int fv = walk(&s, v, o, d, r[6], r[7], flags[i] & 1, &hv, &tv, out + v * S_N);
+            if (v == 4 && g_spec && g_spec_flag) {
+                /* the re-walk of a flagged ray: certified only (its trips go to rewalk) */
+                double st2[S_N];
+                memset(st2, 0, sizeof st2);
+                g_spec = 0;
+                hv = -1;
+                tv = ~0u;
+                fv = walk(&s, v, o, d, r[6], r[7], flags[i] & 1, &hv, &tv, st2);
+                g_spec = 1;
+                g_spec_stat[0] += 1;
+                g_spec_stat[4] += st2[S_WT] + st2[S_LT];
+                g_spec_stat[5] += st2[S_TEST];
+            }
             if (fv != f0 || (f0 && (hv != h0 || tv != t0))) {
                 out[v * S_N + S_BAD] += 1;
                 if (g_bad_n < 64) {

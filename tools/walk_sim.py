@@ -222,6 +222,7 @@ def main():
                 L.walk_sim_camx_bound(int(os.environ.get("WALK_CAMX_BOUND", "0")))
             L.walk_sim_cam.argtypes = [ctypes.c_void_p, ctypes.c_float, ctypes.c_float, ctypes.c_float]
             L.walk_sim_cam(hcam.ctypes.data, *[float(x) for x in eye])
+    L.walk_sim_spec(int(os.environ.get("WALK_SPEC", "0")))
     L.walk_sim_root_only(int(os.environ.get("WALK_ROOT_ONLY", "0")))
     L.walk_sim_axis(int(os.environ.get("WALK_AXIS", "1")))
     L.walk_sim_cull_every(int(os.environ.get("WALK_CULL_EVERY", "0")))
@@ -269,6 +270,11 @@ def main():
             L.walk_sim_camx_stats(P(cx.ctypes.data))
             print("camx per ray: culls won %.3f, excluded-triangle tests %.3f, refused %.4f, checks %.3f"
                   % tuple(v / len(R) for v in cx))
+    if os.environ.get("WALK_SPEC"):
+        sp = np.zeros(8)
+        L.walk_sim_spec_stats(P(sp.ctypes.data))
+        print("speculative cull per ray: flagged %.4f, spec-only culls %.4f, spec-only clip decisions %.4f, "
+              "proven culls %.3f, re-walk trips %.3f, re-walk tests %.3f" % tuple(v / len(R) for v in sp[:6]))
     print(f"config {cfgn}: {len(R)} rays ({sum(flags)} any-hit), {time.time() - t0:.1f} s")
     for v in range(5 if boxes is not None else 3):
         s = {k: round(out[v, i] / len(R), 3) for i, k in enumerate(NAMES)}
