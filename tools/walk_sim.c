@@ -367,6 +367,16 @@ static uint32_t depth_of(uint32_t n0) { uint32_t m = n0 + 1, d = 0; while (m > 1
  * 4 empty leaf visits, 5 tests, 6 pushes, 7 pops, 8 hits, 9 mismatches vs v0 */
 enum { S_WT, S_LT, S_DEC, S_LEAF, S_EMPTY, S_TEST, S_PUSH, S_POP, S_HIT, S_BAD, S_BOXT, S_N };
 
+/* WALK_TRACE: the trip sequence of every ray's v4 walk (0 walking trip, 1 leaf trip),
+ * concatenated in ray order, with each ray's start offset (tools/two_ray_price.py) */
+static uint8_t* g_trace = 0;
+static uint64_t g_trace_cap = 0, g_trace_n = 0;
+static uint64_t* g_trace_off = 0;
+static int g_trace_on = 0;
+void walk_sim_trace(uint8_t* buf, uint64_t cap, uint64_t* off) { g_trace = buf; g_trace_cap = cap; g_trace_off = off; g_trace_n = 0; }
+uint64_t walk_sim_trace_len(void) { return g_trace_n; }
+static void trace_put(int kind) { if (g_trace_on && g_trace_n < g_trace_cap) g_trace[g_trace_n++] = (uint8_t)kind; }
+
 static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int anyhit, float* hd, uint32_t* htri,
                 double* st)
 {
@@ -378,6 +388,7 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
     for (;;) {
         /* one walking trip from `node`: up to three levels */
         st[S_WT] += 1;
+        if (var == 4) trace_put(0);
         int lv = 0, reached_leaf = 0, do_pop = 0;
         float ctn = -INFINITY, ctf = INFINITY;   /* v4 + WALK_CLIP: decisions against the box's interval */
         static int box_every = -1;
@@ -470,6 +481,7 @@ static int walk(const Scene* s, int var, v3 o, v3 d, float tmin, float tmax, int
                             if (miss) { j = e; continue; }
                         }
                         st[S_LT] += 1;
+                        if (var == 4) trace_put(1);
                         for (int k = 0; k < 2 && j < cnt; k++, j++) {
                             float dd;
                             st[S_TEST] += 1;
@@ -555,7 +567,9 @@ int walk_sim(const uint32_t* tree, const float* planes, const uint32_t* ids, con
             g_spec_flag = 0;
             g_tn_c = -INFINITY;
             g_tf_c = INFINITY;
+            if (v == 4 && g_trace) { g_trace_off[i] = g_trace_n; g_trace_on = 1; }
             int fv = walk(&s, v, o, d, r[6], r[7], flags[i] & 1, &hv, &tv, out + v * S_N);
+            g_trace_on = 0;
             if (v == 4 && g_spec && g_spec_flag) {
                 /* the re-walk of a flagged ray: certified only (its trips go to rewalk) */
                 double st2[S_N];

@@ -44,8 +44,11 @@ def main():
     rng = np.random.default_rng(1)
     rays, flags = [], []
     t0 = time.time()
-    for _ in range(nr):
-        x, y = int(rng.integers(cfg.width)), int(rng.integers(cfg.height))
+    # WALK_COHERENT=k: k consecutive samples of each pixel (the kernel's pixel-major units)
+    coh = int(os.environ.get("WALK_COHERENT", "1"))
+    for r_ in range(nr):
+        if r_ % coh == 0:
+            x, y = int(rng.integers(cfg.width)), int(rng.integers(cfg.height))
         o, d = O.camera_ray(u, x, y, float(rng.random()) / cfg.height, float(rng.random()) / cfg.height)
         rays.append([*o, *d, 1e-4, 5000.0])
         flags.append(0)
@@ -231,10 +234,29 @@ def main():
     L.walk_sim_chunk(int(os.environ.get("WALK_CHUNK", "0")), int(os.environ.get("WALK_CHUNK_MIN", "0")),
                      int(os.environ.get("WALK_CHUNK_FREE", "0")),
                      float(np.abs(pos[:, :3]).max()) * 2.0 ** -float(os.environ.get("WALK_MARGIN_LG", "14")))
+    trace = toff = None
+    if os.environ.get("WALK_TRACE"):   # the v4 walk's per-ray trip sequences -> an .npz (two_ray_price.py)
+        trace = np.zeros(len(R) * 4096, np.uint8)
+        toff = np.zeros(len(R) + 1, np.uint64)
+        L.walk_sim_trace(P(trace.ctypes.data), ctypes.c_uint64(trace.size), P(toff.ctypes.data))
     L.walk_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
                P(np.ascontiguousarray(idx).ctypes.data), P(R.ctypes.data), P(F.ctypes.data), ctypes.c_uint32(len(R)),
                P(out.ctypes.data))
     out = out.reshape(5, 11)
+    if trace is not None:
+        L.walk_sim_trace_len.restype = ctypes.c_uint64
+        n = int(L.walk_sim_trace_len())
+        toff[len(R)] = n
+        kind = np.zeros(len(R), np.uint8)   # 0 camera, 1 shadow, 2 bounce (generation order, as WALK_RAYS)
+        i = 0
+        while i < len(R):
+            if i + 2 < len(R) and F[i + 1] == 1:
+                kind[i + 1], kind[i + 2] = 1, 2
+                i += 3
+            else:
+                i += 1
+        np.savez(os.environ["WALK_TRACE"], trace=trace[:n], off=toff, kind=kind)
+        L.walk_sim_trace(None, ctypes.c_uint64(0), None)
     ks = np.array([4, 6, 8, 10, 12, 16], np.uint32)
     tr = np.zeros(4 * len(ks), np.float64)
     L.trail_sim(P(tree.ctypes.data), P(planes.ctypes.data), P(ids.ctypes.data), P(np.ascontiguousarray(pos).ctypes.data),
