@@ -2,8 +2,11 @@
 constant environment) on other meshes, to see how much the bunny stand-in (a near-convex
 displaced sphere: the real bunny.obj is missing from the reference checkout) flatters the
 walk: the reference's own teapot.obj (6,320 triangles; spout, handle and lid make
-concavities and self-shadowing) under its scenes.rs camera, next to the stand-in in the
-same process.  Per mesh and culling mode: the kernel time of one frame (HIP events around
+concavities and self-shadowing) under its scenes.rs camera, and its justElephant.obj
+(12,064 triangles: the only organic, non-convex mesh the checkout holds; no scene of
+scenes.rs uses it, so a three-quarter view framing it like the bunny's, ELEPHANT_CAM),
+next to the stand-in in the same process.  Per mesh and culling mode -- and the HLBVH
+walk (--bvh) -- the kernel time of one frame (HIP events around
 k_path, best of --reps), primary + shadow rays per frame, Mrays/s on the kernel time, the
 bounce rays per primary ray and the trips per ray.  One JSON line per (mesh, mode).
 
@@ -19,6 +22,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 ENV = (0.8, 0.9, 1.0)   # configs.WORKLOADS[3].env's role: a constant environment
+# justElephant.obj spans +-2.4 x +-2.4 x +-4.1 about the origin: a three-quarter view from
+# 21 units with the bunny's camera constant 3.5 (tests/test_gpu_elephant.py uses the same)
+ELEPHANT_CAM = ((15.0, 4.0, 14.0), (0.0, 0.0, 0.0), (0.0, 1.0, 0.0), 3.5)
 
 
 def main():
@@ -26,6 +32,8 @@ def main():
     ap.add_argument("--spp", type=int, default=256)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="4,1,2")
+    ap.add_argument("--bvh", action="store_true", help="also the HLBVH walk (leaf 4) of every mesh")
+    ap.add_argument("--meshes", default="bunny,teapot,elephant")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -33,39 +41,49 @@ def main():
     cfg = importlib.import_module("02562_raytracer_amd.configs")
     sc = importlib.import_module("02562_raytracer_amd.scenes")
     W, H = 1920, 1080
-    meshes = [
-        ("bunny stand-in (config 3)", lambda: cfg.WORKLOADS[3].mesh(), cfg.WORKLOADS[3].camera, cfg.WORKLOADS[3].env),
-        ("teapot.obj (reference asset)", lambda: rt.Mesh.from_obj(os.path.join(cfg.ASSETS, "teapot.obj")),
-         (sc.TEAPOT.eye, sc.TEAPOT.target, sc.TEAPOT.up, sc.TEAPOT.constant), ENV),
-    ]
+    meshes = {
+        "bunny": ("bunny stand-in (config 3)", lambda: cfg.WORKLOADS[3].mesh(), cfg.WORKLOADS[3].camera,
+                  cfg.WORKLOADS[3].env),
+        "teapot": ("teapot.obj (reference asset)", lambda: rt.Mesh.from_obj(os.path.join(cfg.ASSETS, "teapot.obj")),
+                   (sc.TEAPOT.eye, sc.TEAPOT.target, sc.TEAPOT.up, sc.TEAPOT.constant), ENV),
+        "elephant": ("justElephant.obj (reference asset)",
+                     lambda: rt.Mesh.from_obj(os.path.join(cfg.ASSETS, "justElephant.obj")), ELEPHANT_CAM, ENV),
+    }
     names = {0: "off", 1: "certified", 2: "fast", 3: "silhouette", 4: "auto"}
-    for label, make, cam, env in meshes:
+    for key in a.meshes.split(","):
+        label, make, cam, env = meshes[key]
         mesh = make()
         ctx = rt.Context(0)
         ctx.upload_mesh(mesh)
         ctx.upload_bsp(mesh.bsp_tree())
+        if a.bvh:
+            ctx.upload_bvh(mesh.bvh())
         ctx.set_environment(env)
         ctx.set_uniforms(rt.make_uniform(*cam, W, H))
         acc, ids = ctx.alloc(W * H * 16), ctx.alloc(W * H * 4)
-        for mode in [int(m) for m in a.modes.split(",")]:
-            ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, mode)
+        runs = [("BSP", int(m)) for m in a.modes.split(",")] + ([("BVH", None)] if a.bvh else [])
+        for trav, mode in runs:
+            if mode is not None:
+                ctx.set_option(rt._ffi.RT_OPT_BSP_CULL, mode)
             ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 1)
-            c = ctx.render("W9E1", "BSP", (0, 0, W, H), 0, a.spp, acc.ptr, ids.ptr, counts=True)
+            c = ctx.render("W9E1", trav, (0, 0, W, H), 0, a.spp, acc.ptr, ids.ptr, counts=True)
             ctx.set_option(rt._ffi.RT_OPT_DETAIL_COUNTERS, 0)
-            ctx.render("W9E1", "BSP", (0, 0, W, H), 0, a.spp, acc.ptr, ids.ptr)   # warm (and the auto probe)
+            ctx.render("W9E1", trav, (0, 0, W, H), 0, a.spp, acc.ptr, ids.ptr)   # warm (and the auto probe)
             ctx.set_option(rt._ffi.RT_OPT_KERNEL_TIMING, 1)
             best = None
             for _ in range(a.reps):
                 ctx.kernel_time(reset=True)
-                ctx.render("W9E1", "BSP", (0, 0, W, H), 0, a.spp, acc.ptr, ids.ptr)
+                ctx.render("W9E1", trav, (0, 0, W, H), 0, a.spp, acc.ptr, ids.ptr)
                 ms, _n = ctx.kernel_time(reset=True)
                 best = ms if best is None else min(best, ms)
             ctx.set_option(rt._ffi.RT_OPT_KERNEL_TIMING, 0)
             used, pc, ps = ctx.bsp_cull_in_use()
             rays = c["primary"] + c["shadow"]
             print(json.dumps({
-                "mesh": label, "ntris": mesh.ntris, "culling": names[mode],
-                "kernel_in_use": names[used], "probe_ms": [round(pc, 3), round(ps, 3)] if pc else None,
+                "mesh": label, "ntris": mesh.ntris, "traversal": trav,
+                "culling": names[mode] if trav == "BSP" else None,
+                "kernel_in_use": names[used] if trav == "BSP" else None,
+                "probe_ms": [round(pc, 3), round(ps, 3)] if pc and trav == "BSP" else None,
                 "spp": a.spp, "k_path_ms": round(best, 3), "mrays_per_s": round(rays / best / 1e3, 1),
                 "rays": {"primary": c["primary"], "shadow": c["shadow"], "bounce": c["bounce"]},
                 "bounce_per_primary": round(c["bounce"] / max(1, c["primary"]), 4),

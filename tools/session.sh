@@ -74,7 +74,7 @@ for step in "$@"; do
     m5bvh) bash tools/measure.sh $TAG/c5bvh --config 5 --trav BVH --no-cpu-baseline ${M5BVH_OPTS:-} || exit 1 ;;
     meshes)
       # the headline frame's shape on the reference's teapot.obj next to the stand-in (tools/mesh_frame.py)
-      timeout -k 10 600 python tools/mesh_frame.py > $OUT/mesh_frame.json 2> $OUT/mesh_frame.err || { echo "mesh_frame rc=$?"; tail -20 $OUT/mesh_frame.err; exit 1; }
+      timeout -k 10 900 python tools/mesh_frame.py --bvh > $OUT/mesh_frame.json 2> $OUT/mesh_frame.err || { echo "mesh_frame rc=$?"; tail -20 $OUT/mesh_frame.err; exit 1; }
       cat $OUT/mesh_frame.json ;;
     bench:*)
       # one bench line, no profiling: bench:--config,4,--bsp-cull,4
