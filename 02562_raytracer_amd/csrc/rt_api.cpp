@@ -1052,6 +1052,9 @@ int rt_trace_batch(rt_ctx* c, rt_traverse trav, const float* rays_dev, const uin
     if (!c) return RT_E_INVALID;
     if (n == 0) return RT_OK;
     if (!rays_dev || !hits_dev) return fail(c, RT_E_INVALID, "rt_trace_batch: rays and hits are required");
+    // k_trace's shard heads hand out 64-ray blocks below a 2^28 cap: past 2^31 rays the
+    // capped head would keep handing out the same block (and n + 63 overflows near 2^32)
+    if (n >= (1u << 31)) return fail(c, RT_E_INVALID, "rt_trace_batch: n must be below 2^31");
     if (trav != RT_TRAVERSE_BSP) return fail(c, RT_E_UNSUPPORTED, "rt_trace_batch: the BSP walk only");
     if (!c->has_mesh || !c->has_bsp) return fail(c, RT_E_NOT_READY, "rt_trace_batch: no BSP uploaded");
     if (int r = set_dev(c)) return r;

@@ -75,10 +75,6 @@ __device__ __forceinline__ uint32_t lane_v()
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
-typedef float v2f __attribute__((ext_vector_type(2)));
-#ifndef RT_PK_SLAB
-#define RT_PK_SLAB 0
-#endif
 __device__ __forceinline__ float4 as_f4(v4u q)
 {
     return make_float4(__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w));
@@ -201,10 +197,7 @@ struct Pix {
     uint32_t x, y, out;
     bool valid;
 };
-// A/B knob: the tile rows' rotation is (ty * RT_TILE_ROT) mod 8 (1: tiling.tile_of_seq)
-#ifndef RT_TILE_ROT
-#define RT_TILE_ROT 1u
-#endif
+// The tile rows' rotation is ty mod 8 (tiling.tile_of_seq)
 __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint32_t lane)
 {
     Pix p;
@@ -223,7 +216,7 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
         // columns tx = r + ty (mod nranks) when nranks divides 8 and tiles_x
         // (1080p: 240 tile columns); frames under 8 tiles wide are not rotated
         uint32_t t = work * L.nranks + L.rank;
-        uint32_t ty = t / tiles_x, tx = t - ty * tiles_x + (tiles_x >= 8u ? ((ty * RT_TILE_ROT) & 7u) : 0u);
+        uint32_t ty = t / tiles_x, tx = t - ty * tiles_x + (tiles_x >= 8u ? (ty & 7u) : 0u);
         tx = tx >= tiles_x ? tx - tiles_x : tx;
         p.x = tx * 8u + lx;
         p.y = ty * 8u + ly;
@@ -238,7 +231,7 @@ __device__ __forceinline__ Pix map_pixel(const DevLaunch& L, uint32_t work, uint
 __device__ __forceinline__ uint32_t pixel_out(const DevLaunch& L, uint32_t x, uint32_t y)
 {
     if (L.tileset == 0) return (y - L.y0) * L.w + (x - L.x0);
-    const uint32_t ty = y >> 3, tx = x >> 3, r = L.tiles_x >= 8u ? ((ty * RT_TILE_ROT) & 7u) : 0u;
+    const uint32_t ty = y >> 3, tx = x >> 3, r = L.tiles_x >= 8u ? (ty & 7u) : 0u;
     const uint32_t t = ty * L.tiles_x + (tx >= r ? tx - r : tx + L.tiles_x - r);   // map_pixel's s
     return (t - L.rank) / L.nranks * 64u + ((y & 7u) << 3) + (x & 7u);
 }
@@ -291,7 +284,7 @@ __device__ __forceinline__ void pixel_uv(const rt_uniform& u, uint32_t x, uint32
 // bsp_decide).
 // CULL: the back-face culling test of w9e3.wgsl:328 (|denom| < 5e-5 or
 // denom > 0 rejects) in place of |denom| < 1e-10.
-// BARY false (the walks' trip loops with RT_LAZY_BARY): the barycentrics are
+// BARY false (the walks' trip loops): the barycentrics are
 // not returned, and a candidate whose approximate quotients already settle
 // every condition of the accept predicate (beta and gamma non-negative by the
 // sign of a*r and b*r, their sum below 1 and the distance inside [tmin, tmax]
@@ -344,12 +337,9 @@ __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const
     gamma = b / denom;
     return !((beta < 0.0f) | (gamma < 0.0f) | (beta + gamma > 1.0f) | (dist > tmax) | (dist < tmin));
 }
-#ifndef RT_LAZY_BARY
-#define RT_LAZY_BARY 1
-#endif
 // beta and gamma of the accepted record at byte offset k of the walk's buffer
 // for the ray (o, w): intersect_triangle's a / denom and b / denom with the
-// operations of tri_math (the trip loop does not keep them, RT_LAZY_BARY)
+// operations of tri_math (the trip loops do not keep them)
 template <int TRAV>
 __device__ __forceinline__ void bary_of(const DevScene& S, uint32_t k, const f3 o, const f3 w, float& beta,
                                         float& gamma)
@@ -464,16 +454,11 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 // stores the current tmax into the depth-dep slot unconditionally: no pending
 // entry lives at a depth >= depth(m) (they are all ancestors of m), so the
 // store is dead unless the trail bit is set.
-// RT_TRAIL_SLOT 1: the walk derives the trail slot of its first level once per
-// trip and the next levels' slots as constant offsets from it (ds_write
-// immediate offsets), and sets the trail bit with one shift-or.
-#ifndef RT_TRAIL_SLOT
-#define RT_TRAIL_SLOT 1
-#endif
-// RT_DECIDE_EXACT 1: every decision divides out the exact t (A/B knob)
-#ifndef RT_DECIDE_EXACT
-#define RT_DECIDE_EXACT 1
-#endif
+// The walk derives the trail slot of its first level once per trip and the next
+// levels' slots as constant offsets from it (ds_write immediate offsets; `stk` is
+// this level's slot), and sets the trail bit with one shift-or.  Every decision
+// divides out the exact t (the wave runs the exact path in nearly every trip
+// anyway: 28 % of decisions need it), with no approximate test first.
 template <bool COUNT>
 __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, uint32_t dep, const f3 o,
                                                const f3 d, const f3 inv, Trav& t, Counters& c, float lo, float& hi)
@@ -483,60 +468,25 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     const float ao = comp(o, axis), iv = comp(inv, axis);
     const uint32_t near_node = 2u * m + (__float_as_uint(iv) >> 31);   // see bsp_inv1
     const float x = __uint_as_float(n.y) - ao;
-    if (RT_DECIDE_EXACT) {
-        // every lane divides out the exact t (the wave runs the exact path in
-        // nearly every trip anyway: 28 % of decisions need it), no approximate test
-        if (COUNT) c.v[C_EXACT_NODES]++;
-        const float ad = comp(d, axis);
-        const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
-        float tt = rt_div_by_recip(x, denom, iv);
-        if (!(rt_div_by_recip_ok(x) & (iv == iv))) {
-            asm volatile("");   // keep the rare IEEE division behind its branch (no if-conversion)
-            tt = x / denom;
-        }
-        // against [lo, hi]: the ray interval, clipped to the treelet root's
-        // content box (RT_BSP_CLIP); a plane beyond it leaves one side hitless
-        const bool cnear = tt > hi;
-        const bool gofar = (!cnear) & (tt < lo);
-        const bool push = (!cnear) & !(tt < lo);
-        if (RT_TRAIL_SLOT) {
-            stk[0] = t.tmax;
-            t.lvl |= (uint32_t)push << dep;
-        } else {
-            stk[dep * 256u] = t.tmax;
-            t.lvl |= push ? 1u << dep : 0u;
-        }
-        t.tmax = push ? tt : t.tmax;
-        hi = push ? tt : hi;
-        return gofar ? near_node ^ 1u : near_node;
+    if (COUNT) c.v[C_EXACT_NODES]++;
+    const float ad = comp(d, axis);
+    const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
+    // RN(x / denom) from the per-ray RN(1/denom) (include/rt_detmath.h); the IEEE
+    // division outside its operand range or for a NaN-flagged axis
+    float tt = rt_div_by_recip(x, denom, iv);
+    if (!(rt_div_by_recip_ok(x) & (iv == iv))) {
+        asm volatile("");   // keep the rare IEEE division behind its branch (no if-conversion)
+        tt = x / denom;
     }
-    const float tq = x * iv;
-    const float mg = __builtin_fmaf(rt_absf(tq), 0x1p-20f, 1e-30f);   // exact product: = mul + add
-    // (bitwise & | on bools: no short-circuit control flow)
-    const bool cnear = tq - mg > t.tmax;                                   // certainly t > tmax
-    const bool cfar = (!cnear) & (tq + mg < t.tmin) & (tq + mg <= t.tmax);   // certainly !(t > tmax) && t < tmin
-    const bool amb = (!cnear) & (!cfar);
-    float tt = tq;
-    if (amb) {
-        if (COUNT) c.v[C_EXACT_NODES]++;
-        const float ad = comp(d, axis);
-        const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
-        // RN(x / denom) from the per-ray RN(1/denom) (include/rt_detmath.h);
-        // IEEE division outside its operand range or for a NaN-flagged axis
-        if (rt_div_by_recip_ok(x) & (iv == iv)) tt = rt_div_by_recip(x, denom, iv);
-        else tt = x / denom;
-    }
-    const bool inside = amb & !(tt > t.tmax);
-    const bool gofar = cfar | (inside & (tt < t.tmin));
-    const bool push = inside & !(tt < t.tmin);
-    if (RT_TRAIL_SLOT) {
-        stk[0] = t.tmax;   // stk: this level's slot (bsp_walk)
-        t.lvl |= (uint32_t)push << dep;
-    } else {
-        stk[dep * 256u] = t.tmax;   // the tmax its pop restores
-        t.lvl |= push ? 1u << dep : 0u;
-    }
+    // against [lo, hi]: the ray interval, clipped to the treelet root's content
+    // box (bsp_box_miss); a plane beyond it leaves one side hitless
+    const bool cnear = tt > hi;
+    const bool gofar = (!cnear) & (tt < lo);
+    const bool push = (!cnear) & !(tt < lo);
+    stk[0] = t.tmax;   // the tmax its pop restores
+    t.lvl |= (uint32_t)push << dep;
     t.tmax = push ? tt : t.tmax;
+    hi = push ? tt : hi;
     return gofar ? near_node ^ 1u : near_node;
 }
 
@@ -566,9 +516,6 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 // more round trip; loading them with the trip's loads was no faster then,
 // profiles/r03/ab_pre_c*.txt.  The 96-B treelets of the certified culling load
 // them anyway.)
-#ifndef RT_LEAF_TESTS
-#define RT_LEAF_TESTS 2   // triangle tests per leaf trip of the BSP walk: 1 or 2
-#endif
 template <bool COUNT, bool CULL, class LOG>
 __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const v4u r1, const v4u q5,
                                                const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c, LOG& lg)
@@ -582,7 +529,7 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
             c.v[C_TESTS]++;
         }
         float dist, beta, gamma;
-        if (tri_math<true, COUNT, CULL, !RT_LAZY_BARY>(as_f4(nx), as_f4(r1), as_f4(r2), o, d, t.tmin, t.tmax, dist,
+        if (tri_math<true, COUNT, CULL, false>(as_f4(nx), as_f4(r1), as_f4(r2), o, d, t.tmin, t.tmax, dist,
                                                        beta, gamma, &c)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
@@ -590,17 +537,13 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
             // an any-hit walk keeps the hit it started from (k_path redraws from
             // it); selects, not a branch (no exec-mask work in the trip)
             t.hit_k = anyhit ? t.hit_k : t.leaf_k;
-            if (!RT_LAZY_BARY) {
-                t.beta = anyhit ? t.beta : beta;
-                t.gamma = anyhit ? t.gamma : gamma;
-            }
         }
         t.leaf_k += 48u;
     }
 }
 
-// The leaf half of a BSP trip: test the record in q0..q2 (and, with
-// RT_LEAF_TESTS 2, the next one, whose first 16 B are q3).
+// The leaf half of a BSP trip: test the record in q0..q2 and the next one,
+// whose 48 B are q3..q5.
 template <bool COUNT, bool CULL, class LOG>
 __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, const v4u q0, const v4u q1, const v4u q2,
                                                const v4u q3, const v4u q4, const v4u q5, const f3 o, const f3 d, bool anyhit, Trav& t,
@@ -612,19 +555,15 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
         c.v[C_TESTS]++;
     }
     float dist, beta, gamma;
-    if (tri_math<true, COUNT, CULL, !RT_LAZY_BARY>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta,
+    if (tri_math<true, COUNT, CULL, false>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta,
                                                    gamma, &c)) {
         if (COUNT) c.v[C_ACCEPTS]++;
         t.tmax = dist;
         t.found = true;
         t.hit_k = anyhit ? t.hit_k : t.leaf_k;
-        if (!RT_LAZY_BARY) {
-            t.beta = anyhit ? t.beta : beta;
-            t.gamma = anyhit ? t.gamma : gamma;
-        }
     }
     t.leaf_k += 48u;
-    if (RT_LEAF_TESTS > 1) leaf_test_next<COUNT, CULL>(rs, q3, q4, q5, o, d, anyhit, t, c, lg);
+    leaf_test_next<COUNT, CULL>(rs, q3, q4, q5, o, d, anyhit, t, c, lg);
     const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
     done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
     pop = leaf_done & !t.found;
@@ -656,21 +595,22 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 //    ray has that coordinate o_a exactly, so the slab is a yes/no test of o_a
 //    against the grown box -- inv * inf makes its products +-inf (o_a outside:
 //    both ends of the slab at +inf or at -inf, the interval is empty; inside:
-//    -inf..+inf, no constraint; a zero product is NaN and constrains nothing).
-//    An infinite end culls against the gap tolerance's cap S.bsp_cull_emax
-//    (FLT_MAX; +inf with culling off).  W9E1's shadow rays (0, 1, 0)
-//    (w9e1.wgsl:442-446) are the common case;
+//    -inf..+inf, no constraint).  An infinite end culls against the gap
+//    tolerance's cap S.bsp_cull_emax (FLT_MAX; +inf with culling off).  W9E1's
+//    shadow rays (0, 1, 0) (w9e1.wgsl:442-446) are the common case.  On the grown
+//    box's face itself (RN(dl - m) == 0 or RN(dh + m) == 0) that end's product is
+//    0 x inf = NaN, fminf / fmaxf take the other end (+-inf) and the subtree is
+//    culled: the closed face counts as outside, and so may o_a within the two
+//    roundings of dl - m (a few ulps of the coordinates) inside it.  That is exact
+//    because the certified margin carries slack beyond its bound: its 2u D1 and
+//    2^-19 max(|o|inf, scene) terms exceed the proven L-inf distance of any
+//    accepted hit point from its triangle's box by far more than those ulps, so no
+//    point within them of the grown face can be an accept.  (The fast margin is
+//    not a bound either way.);
 //  * nonzero, |w_a| <= 1e-8 (inv is the NaN flag): constrains nothing, the NaN
 //    drops out of fminf / fmaxf.
-// RT_BSP_CULL 0 compiles the test out (A/B builds; RT_OPT_BSP_CULL then has no effect).
-#ifndef RT_BSP_CULL
-#define RT_BSP_CULL 1
-#endif
-// RT_BSP_CLIP 1: the trip's decisions also use the interval clipped to the box
-// (bsp_walk; DESIGN.md section 4 "Subtree culling")
-#ifndef RT_BSP_CLIP
-#define RT_BSP_CLIP 1
-#endif
+// The trip's decisions also use the interval clipped to the box (bsp_walk;
+// DESIGN.md section 4 "Subtree culling").
 // The gap factor `gap` is DevScene.bsp_cull_gap: 2^-18, or +inf with culling
 // off (no gap exceeds an infinite threshold; 0 x inf = NaN compares false).
 // Off is data, not a branch on a uniform flag: a uniform bool kept as a lane
@@ -678,32 +618,6 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
 // compiler (k_direct's shadow walk culled in the lanes that had been inactive
 // where the mask was computed; tests/test_gpu_cull.py caught it).  The mode
 // is data for the same reason (DevScene cull_k1 / cull_k3 / cull_ko).
-#ifndef RT_SHADE_PRIO
-#define RT_SHADE_PRIO 0
-#endif
-#ifndef RT_W7E3_SHADE_PRIO
-#define RT_W7E3_SHADE_PRIO 2
-#endif
-#ifndef RT_AB_NO_CONE
-#define RT_AB_NO_CONE 0
-#endif
-#ifndef RT_AB_EXTRA_LIVE
-#define RT_AB_EXTRA_LIVE 0
-#endif
-#ifndef RT_AB_CULL_FORMULA
-#define RT_AB_CULL_FORMULA 0
-#endif
-#ifndef RT_AB_CULL_CAM
-#define RT_AB_CULL_CAM 1
-#endif
-// A/B probes only: the silhouette instantiation without its node-data load (zeros) or
-// without its arithmetic (the certified camera term)
-#ifndef RT_AB_SIL_NOLOAD
-#define RT_AB_SIL_NOLOAD 0
-#endif
-#ifndef RT_AB_SIL_NOMATH
-#define RT_AB_SIL_NOMATH 0
-#endif
 __device__ __forceinline__ float h2f(uint32_t bits) { return (float)__builtin_bit_cast(_Float16, (uint16_t)bits); }
 // CM 0: the fast margin's formula alone, m = max(|o|inf ko, dscene), for a
 // context whose culling is not certified (the host picks k_path's
@@ -718,7 +632,7 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
                                              const f3 o, const f3 w, const f3 inv, float tmin, float tmax, float& lo,
                                              float& hi)
 {
-    constexpr bool FULL = CM >= 1 && RT_AB_CULL_FORMULA != 1;   // (RT_AB_CULL_FORMULA 1: A/B only)
+    constexpr bool FULL = CM >= 1;
     const float oo[3] = {o.x, o.y, o.z}, iv[3] = {inv.x, inv.y, inv.z};
     // vectors from the origin to the box's faces; D1 bounds |v0 - o|_1 over the box
     float dl[3], dh[3], D1 = 0.0f;
@@ -747,7 +661,7 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
                                                        __builtin_fmaf(rt_absf(w.x), h2f(q5.z >> 16), 0.0f)));
         const float dlb2 = rt_absf(wc) - wr;
         float den = __uint_as_float(q5.x << 16);
-        if (!RT_AB_NO_CONE) den = __builtin_fmaxf(den, dlb2 - (20.0f * 0x1p-24f) * w1);   // (A/B knob: without it)
+        den = __builtin_fmaxf(den, dlb2 - (20.0f * 0x1p-24f) * w1);
         // a camera ray (its origin is the eye the treelets' camera terms are for):
         // |denom| / E_T^2 >= G |w|inf, G (f16) precomputed per treelet for the eye
         // (k_treelet_hcam; DESIGN.md section 4 "Certified culling", the camera bound)
@@ -755,7 +669,7 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
         const float winf = __builtin_fmaxf(__builtin_fmaxf(rt_absf(w.x), rt_absf(w.y)), rt_absf(w.z));
         const float dcam = __builtin_fmaf(winf, h2f(q5.x >> 16), 0.0f);   // G: f16 in the high half
         float dc = dcam;
-        if constexpr (CM == 2 && !RT_AB_SIL_NOMATH) {
+        if constexpr (CM == 2) {
             // RT_BSP_CULL_SILHOUETTE: the subtree's two triangles of smallest camera
             // term are bounded per ray by their own normals x = n*/E_t^2 (f16, q6; NaN
             // slots drop out of the minimum), the rest by G_x (q6.w): |denom| / E_t^2
@@ -767,24 +681,11 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
             const float dx = __builtin_fmaf(-0x1p-9f, w1, __builtin_fminf(rt_absf(x0), rt_absf(x1)));
             dc = __builtin_fmaxf(dcam, __builtin_fminf(dx, __builtin_fmaf(winf, h2f(q6.w & 0xFFFFu), 0.0f)));
         }
-        if (RT_AB_CULL_CAM) den = __builtin_fmaxf(den, cam ? dc : 0.0f);
+        den = __builtin_fmaxf(den, cam ? dc : 0.0f);
         // (fused: fewer roundings than the proof's constants allow for)
         m = __builtin_fmaf(D1, __builtin_fmaf(S.cull_k1 * w1, __builtin_amdgcn_rcpf(den), S.cull_k3), m);
     }
     float tn = tmin, tf = tmax;
-#if RT_PK_SLAB
-    // the slab pairs as packed f32 (v_pk_add_f32 / v_pk_mul_f32: two lanes' worth
-    // per issue; the same IEEE operations as the scalar form)
-    const v2f mm = {-m, m};
-#pragma unroll
-    for (int a = 0; a < 3; a++) {
-        const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : iv[a] * __builtin_inff();
-        const v2f dd = {dl[a], dh[a]};
-        const v2f t = (dd + mm) * ib;
-        tn = __builtin_fmaxf(tn, __builtin_fminf(t.x, t.y));
-        tf = __builtin_fminf(tf, __builtin_fmaxf(t.x, t.y));
-    }
-#else
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : iv[a] * __builtin_inff();   // +1e8: a zero component
@@ -792,13 +693,12 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
         tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
         tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
     }
-#endif
     // a clear gap: the rounding of the slab products cannot close it
     // (capped: an infinite slab end from a zero direction component must still
     // show a gap; a finite product cannot reach the cap)
     const float e = __builtin_fminf((rt_absf(tn) + rt_absf(tf)) * S.bsp_cull_gap, S.bsp_cull_emax);
     // the interval the subtree's content can be hit in, widened by the same
-    // tolerance (RT_BSP_CLIP; culling off: e = inf or NaN, lo = tmin, hi = tmax)
+    // tolerance (culling off: e = inf or NaN, lo = tmin, hi = tmax)
     lo = __builtin_fmaxf(tmin, tn - e);
     hi = __builtin_fminf(tmax, tf + e);
     // an empty subtree's content box is +inf / -inf (its slabs are NaN, never a
@@ -819,34 +719,30 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
                                          const f3 inv, Trav& t, Counters& c, bool& pop)
 {
     uint32_t m = t.node;
-    float lo = t.tmin, hi = t.tmax;   // the decisions' interval
-    if (RT_BSP_CULL) {
-        float blo, bhi;
-        if (bsp_box_miss<CM>(S, q0, q1, q5, q6, o, d, inv, t.tmin, t.tmax, blo, bhi)) {
-            if (COUNT) c.v[C_CULLS]++;
-            pop = true;
-            return false;
-        }
-        if (RT_BSP_CLIP) {
-            lo = blo;
-            hi = bhi;
-        }
+    float lo = t.tmin, hi = t.tmax;   // the decisions' interval: [tmin, tmax] clipped to the box
+    float blo, bhi;
+    if (bsp_box_miss<CM>(S, q0, q1, q5, q6, o, d, inv, t.tmin, t.tmax, blo, bhi)) {
+        if (COUNT) c.v[C_CULLS]++;
+        pop = true;
+        return false;
     }
+    lo = blo;
+    hi = bhi;
     const uint32_t dep = heap_depth(m);
     uint2 n = make_uint2(q1.z, q1.w);
     bool leaf = (n.x & 3u) == 3u;
     if (!leaf) {
-        // the trail slot of this level (RT_TRAIL_SLOT), or the trail base
-        float* const s0 = RT_TRAIL_SLOT ? stk + dep * 256u : stk;
+        // the trail slot of this level
+        float* const s0 = stk + dep * 256u;
         m = bsp_decide<COUNT>(s0, n, m, dep, o, d, inv, t, c, lo, hi);
         n = (m & 1u) ? make_uint2(q2.z, q2.w) : make_uint2(q2.x, q2.y);
         leaf = (n.x & 3u) == 3u;
         if (!leaf) {
-            m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 256 : stk, n, m, dep + 1u, o, d, inv, t, c, lo, hi);
+            m = bsp_decide<COUNT>(s0 + 256, n, m, dep + 1u, o, d, inv, t, c, lo, hi);
             const v4u g = (m & 2u) ? q4 : q3;
             n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
             leaf = (n.x & 3u) == 3u;
-            if (!leaf) m = bsp_decide<COUNT>(RT_TRAIL_SLOT ? s0 + 512 : stk, n, m, dep + 2u, o, d, inv, t, c, lo, hi);
+            if (!leaf) m = bsp_decide<COUNT>(s0 + 512, n, m, dep + 2u, o, d, inv, t, c, lo, hi);
         }
     }
     t.node = m;
@@ -888,15 +784,9 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
         // array, so its load returns zeros without a memory access (zeros give
         // dc = dcam, and a non-camera ray ignores dc) -- the secondary rays of a
         // large scene do not stream the array
-        uint32_t off6 = t.node * 16u;
-#ifndef RT_SIL_MASKED
-#define RT_SIL_MASKED 1
-#endif
-        if (RT_SIL_MASKED) {
-            const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
-            off6 = (!in_leaf & cam) ? off6 : 0x80000000u;
-        }
-        if (!RT_AB_SIL_NOLOAD) q6 = __builtin_amdgcn_raw_buffer_load_b128(rs6, off6, 0, 0);
+        const bool cam = (o.x == S.cam_eye[0]) & (o.y == S.cam_eye[1]) & (o.z == S.cam_eye[2]);
+        const uint32_t off6 = (!in_leaf & cam) ? t.node * 16u : 0x80000000u;
+        q6 = __builtin_amdgcn_raw_buffer_load_b128(rs6, off6, 0, 0);
         asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5), "+v"(q6));
     } else {
         asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3), "+v"(q4), "+v"(q5));
@@ -907,23 +797,8 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
             c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
     }
     bool done = false, pop = false;
-#if RT_AB_EXTRA_LIVE
-    // A/B probe only (DESIGN.md section 4 "Round 4"): RT_AB_EXTRA_LIVE more values
-    // live across both halves of the trip, the registers a wave-cooperative leaf
-    // test needs for a helper lane's copy of its owner's ray (o, w, tmin, tmax)
-    float xl[RT_AB_EXTRA_LIVE];
-#pragma unroll
-    for (int i = 0; i < RT_AB_EXTRA_LIVE; i++) {
-        xl[i] = i < 3 ? comp(o, i) : i < 6 ? comp(d, i - 3) : i == 6 ? t.tmin : t.tmax;
-        asm volatile("" : "+v"(xl[i]));
-    }
-#endif
     if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg);
     else bsp_walk<COUNT, CM>(S, stk, q0, q1, q2, q3, q4, q5, q6, o, d, inv, t, c, pop);
-#if RT_AB_EXTRA_LIVE
-#pragma unroll
-    for (int i = 0; i < RT_AB_EXTRA_LIVE; i++) asm volatile("" : : "v"(xl[i]));
-#endif
     if (pop) done = bsp_pop(stk, t);
     return done;
 }
@@ -961,10 +836,6 @@ __device__ __forceinline__ f3 bsp_inv(const f3 d) { return V(bsp_inv1(d.x), bsp_
 // intersect_bvh + intersect_bb2, bvh.wgsl:154-191 / 16-83: slab test in axis
 // order y, x, z on [0, 1e27] (ray interval ignored), right child popped first,
 // 1000-pop cap, WGSL index clamping of the 50-entry stack.  One pop per call.
-#ifndef RT_BB2_BRANCHFREE
-#define RT_BB2_BRANCHFREE 1
-#endif
-#if RT_BB2_BRANCHFREE
 // The same predicate without control flow: the swaps and bound updates are
 // selects with the shader's comparisons (NaN compares false, as its ifs do).
 // The early `return false` after an axis needs no flag: t0 only grows and t1
@@ -986,29 +857,6 @@ __device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, co
     bb2_axis(nr.z, fr.z, t0, t1);
     return !(t0 > t1);
 }
-#else
-__device__ __forceinline__ bool bb2(const f3 inv, const f3 o, const float4 a, const float4 b)
-{
-    float t0 = 0.0f, t1 = 1e27f;
-    const f3 nr = mul(sub(V(a.x, a.y, a.z), o), inv);
-    const f3 fr = mul(sub(V(b.x, b.y, b.z), o), inv);
-    float tn = nr.y, tf = fr.y;
-    if (tn > tf) { float s = tn; tn = tf; tf = s; }
-    if (tn > t0) t0 = tn;
-    if (tf < t1) t1 = tf;
-    if (t0 > t1) return false;
-    tn = nr.x; tf = fr.x;
-    if (tn > tf) { float s = tn; tn = tf; tf = s; }
-    if (tn > t0) t0 = tn;
-    if (tf < t1) t1 = tf;
-    if (t0 > t1) return false;
-    tn = nr.z; tf = fr.z;
-    if (tn > tf) { float s = tn; tn = tf; tf = s; }
-    if (tn > t0) t0 = tn;
-    if (tf < t1) t1 = tf;
-    return !(t0 > t1);
-}
-#endif
 
 // BVH stack split: entries [0, K) in LDS ([slot][thread], 4 B), entries [K, 50)
 // in a per-lane global region ([slot - K][lane] across the grid) -- a walk
@@ -1043,10 +891,6 @@ __device__ __forceinline__ void bvh_init(Trav& t, float tmin, float tmax)
 // Stack slot of entry i under WGSL index clamping (bvh.wgsl:134-137: node_stack[50]).
 __device__ __forceinline__ uint32_t bvh_slot(uint32_t i) { return i < 50u ? i : 49u; }
 
-#ifndef RT_BVH_TWO_POP
-#define RT_BVH_TWO_POP 1
-#endif
-
 // One trip of a lane through intersect_bvh (bvh.wgsl:154-191), one memory
 // round trip: a lane inside a leaf tests one triangle (its 48-B record), a
 // lane between leaves pops one node (32-B record) and slab-tests it.  The
@@ -1064,7 +908,6 @@ __device__ __forceinline__ bool bvh_step_log(const DevScene& S, uint32_t* stk, c
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bvh_base, (short)0, (int)S.bvh_bytes, 0x00020000);
     const bool in_leaf = t.leaf_k != t.leaf_end;
-#if RT_BVH_TWO_POP
     // a walking lane loads the records of the top two stack entries: when the
     // first misses, the second is the next pop and is handled in the same trip
     const uint32_t base = in_leaf ? t.leaf_k : t.tos;
@@ -1074,13 +917,6 @@ __device__ __forceinline__ bool bvh_step_log(const DevScene& S, uint32_t* stk, c
     v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base2, 0, 0);
     v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rs, base2 + 16u, 0, 0);
     asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2), "+v"(q3));
-#else
-    const uint32_t base = in_leaf ? t.leaf_k : t.tos;
-    v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
-    v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
-    v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 32u, 0, 0);
-    asm volatile("" : "+v"(q0), "+v"(q1), "+v"(q2));
-#endif
     if (in_leaf) {
         lg.tested(t.leaf_k);
         if (COUNT) {
@@ -1089,7 +925,7 @@ __device__ __forceinline__ bool bvh_step_log(const DevScene& S, uint32_t* stk, c
         }
         float dist, beta, gamma;
         // the BVH walk never narrows the ray interval: both bounds are exact
-        if (tri_math<true, COUNT, CULL, !RT_LAZY_BARY>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist,
+        if (tri_math<true, COUNT, CULL, false>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist,
                                                        beta, gamma, &c)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
@@ -1097,15 +933,10 @@ __device__ __forceinline__ bool bvh_step_log(const DevScene& S, uint32_t* stk, c
             // an any-hit walk keeps the hit it started from (k_path redraws from
             // it); selects, not a branch (no exec-mask work in the trip)
             t.hit_k = anyhit ? t.hit_k : t.leaf_k;
-            if (!RT_LAZY_BARY) {
-                t.beta = anyhit ? t.beta : beta;
-                t.gamma = anyhit ? t.gamma : gamma;
-            }
         }
         t.leaf_k += 48u;
         if (anyhit & t.found) return true;
     } else {
-#if RT_BVH_TWO_POP
         // Stack invariant: tos = entry node-1, tos2 = entry node-2 (clamped
         // slots), so both reads the reference does after a push are exact.
         // Box tests have no side effect (the slab test ignores the ray
@@ -1144,28 +975,6 @@ __device__ __forceinline__ bool bvh_step_log(const DevScene& S, uint32_t* stk, c
             if (t.node != 0u) t.tos = reload ? bvh_ld(stk, dp, bvh_slot(t.node - 1u)) : t.tos2;
             if (t.node >= 2u) t.tos2 = bvh_ld(stk, dp, bvh_slot(t.node - 2u));
         }
-#else
-        if (COUNT) c.v[C_POPS]++;
-        t.lvl++;
-        t.node--;
-        const uint32_t cur = t.tos;
-        const float4 a = as_f4(q0), b = as_f4(q1);
-        const bool hit = bb2(inv, o, a, b);
-        const uint32_t w0 = q0.w, w1 = q1.w;
-        if (hit & (w1 != 0u)) {   // leaf: its triangles from the next trip on
-            t.leaf_k = w0;
-            t.leaf_end = w0 + w1;
-        }
-        if (hit & (w1 == 0u)) {   // interior: push left (cur + 1), then right
-            bvh_st(stk, dp, t.node < 50u ? t.node : 49u, cur + 32u);
-            t.node++;
-            bvh_st(stk, dp, t.node < 50u ? t.node : 49u, w0);
-            t.node++;
-            t.tos = w0;
-        } else if (t.node != 0u) {
-            t.tos = bvh_ld(stk, dp, t.node - 1u < 50u ? t.node - 1u : 49u);
-        }
-#endif
     }
     return (t.leaf_k == t.leaf_end) & ((t.lvl >= 1000u) | (t.node == 0u));
 }
@@ -1212,7 +1021,7 @@ __device__ __forceinline__ bool trace(const DevScene& S, void* stk, const BvhDee
     const f3 inv = trav_inv<TRAV>(d);
     for (uint32_t guard = 0; guard < (1u << 24); guard++)
         if (trav_step<TRAV, COUNT>(S, stk, dp, o, d, inv, anyhit, t, c)) break;
-    if (RT_LAZY_BARY && t.found && !anyhit) bary_of<TRAV>(S, t.hit_k, o, d, t.beta, t.gamma);
+    if (t.found && !anyhit) bary_of<TRAV>(S, t.hit_k, o, d, t.beta, t.gamma);
     out = trav_out(t);
     return t.found;
 }
@@ -1349,9 +1158,6 @@ enum { PH_NEW = 0, PH_CLOSEST = 1, PH_SHADOW = 2 };
 // registers except the hit record of an accept, and the spills sit in the
 // shading code).  Measured at 256 spp: 5 waves 2744, 6: 2897, 7: 3029,
 // 8: 3084 Mrays/s.
-#ifndef RT_ENV_TEX
-#define RT_ENV_TEX 1
-#endif
 // BVH instantiations: 8 waves/SIMD (64 VGPRs).  Round 1 measured 7 best
 // (3007 Mrays/s vs 2712 at 8); with the SLP-free build and four steps per
 // check 8 wins: 5792 vs 5667 (7) and 5511 (6) (profiles/r02/ab_waves2.txt)
@@ -1461,7 +1267,7 @@ template <int MODE>
 __device__ __forceinline__ f3 env_at(const DevLaunch& L, const f3 env, const f3 d)
 {
     f3 e = env;
-    if (RT_ENV_TEX && L.env_tex) {
+    if (L.env_tex) {
         float rgb[3];
         const uint32_t w = sopaque(L.env_w), h = sopaque(L.env_h);   // see make_cam_opaque
         if (MODE == RT_MODE_W9E2) rt_det_env_sample_rgbe(L.env_tex, w, h, d.x, d.y, d.z, rgb);
@@ -1608,7 +1414,7 @@ k_path(DevScene S, DevLaunch L)
     constexpr uint32_t MAXD = W8E1 ? 10u : 50u;
     // the shading phase's issue priority (W7E3's short Cornell-box rays shade often:
     // +0.9 % at 2, profiles/r04/ab_shade_prio.txt; neutral on W9E1's configs)
-    constexpr int SPRIO = MODE == RT_MODE_W7E3 ? RT_W7E3_SHADE_PRIO : RT_SHADE_PRIO;
+    constexpr int SPRIO = MODE == RT_MODE_W7E3 ? 2 : 0;
     // W9E1 draws the next bounce direction after the shadow walk, from the hit
     // the any-hit walk left in the traversal state (resolve() again): the shadow
     // walk draws no random numbers, so the PRNG sequence is the reference's, and
@@ -1738,8 +1544,8 @@ k_path(DevScene S, DevLaunch L)
             tstamp = now;
         }
         {
-        // (A/B: RT_SHADE_PRIO raises the wave's issue priority for its shading and refill
-        // phase, so lanes are refilled sooner while the other waves trace)
+        // (SPRIO raises the wave's issue priority for its shading and refill phase,
+        // so lanes are refilled sooner while the other waves trace)
         if (SPRIO) __builtin_amdgcn_s_setprio(SPRIO);
         // the shading and refill phases read the kernel arguments afresh (kreload)
         const DevScene& Sk = kreload<DevScene>(KARG_S);
@@ -1758,7 +1564,7 @@ k_path(DevScene S, DevLaunch L)
             if (!shadow) {
                 if (tr.found) {
                     // the hit's barycentrics, kept in tr across a shadow walk (REDRAW)
-                    if (RT_LAZY_BARY) bary_of<TRAV>(S, tr.hit_k, ro, rd, tr.beta, tr.gamma);
+                    bary_of<TRAV>(S, tr.hit_k, ro, rd, tr.beta, tr.gamma);
                     const HitRec h = resolve<TRAV, W9E3>(S, trav_out(tr), ro, rd, !W9);
                     if (bounce == 0) prim = h.tri;
                     const rt_material& m = mat_of(S, h.material);
@@ -2329,7 +2135,7 @@ __global__ void __launch_bounds__(256) k_query(DevScene S, const float* rays, co
         const uint32_t slot = (t.hit_k - (TRAV == RT_TRAVERSE_BVH ? S.bvh_rec_off : S.bsp_rec_off)) / 48u;
         h.tri = !t.found ? 0xFFFFFFFFu : anyhit ? lg.last : (TRAV == RT_TRAVERSE_BVH ? S.bvh_ids : S.bsp_ids)[slot];
         h.dist = t.found ? t.tmax : 0.0f;
-        if (RT_LAZY_BARY && t.found && !anyhit) bary_of<TRAV>(S, t.hit_k, o, d, t.beta, t.gamma);
+        if (t.found && !anyhit) bary_of<TRAV>(S, t.hit_k, o, d, t.beta, t.gamma);
         h.beta = t.found && !anyhit ? t.beta : 0.0f;
         h.gamma = t.found && !anyhit ? t.gamma : 0.0f;
         h.ntested = lg.n;
@@ -2764,7 +2570,7 @@ __global__ void __launch_bounds__(256) k_unpack(uint32_t W, uint32_t H, uint32_t
         // t: the sequence position (map_pixel: rows rotated by their index mod 8)
         const uint32_t t = (uint32_t)(g >> 6), lane = (uint32_t)(g & 63u);
         const uint32_t ty = t / tiles_x;
-        uint32_t tx = t - ty * tiles_x + (tiles_x >= 8u ? ((ty * RT_TILE_ROT) & 7u) : 0u);
+        uint32_t tx = t - ty * tiles_x + (tiles_x >= 8u ? (ty & 7u) : 0u);
         tx = tx >= tiles_x ? tx - tiles_x : tx;
         const uint32_t x = tx * 8u + (lane & 7u), y = ty * 8u + (lane >> 3);
         if (x >= W || y >= H) continue;

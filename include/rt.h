@@ -479,7 +479,8 @@ int rt_gather_tiles(rt_ctx* ctx, uint32_t width, uint32_t height, const float* l
  * culling mode).  Asynchronous on the context stream; timed by
  * RT_OPT_KERNEL_TIMING like the render kernels.  RT_OPT_SHADE_THRESHOLD's low
  * byte (default 16) is the lanes-still-tracing count at which finished lanes
- * refill.  DESIGN.md section 4 "Outside the megakernel".
+ * refill.  n must stay below 2^31 (the per-XCD work queues count 64-ray blocks in
+ * 32-bit heads; RT_E_INVALID above).  DESIGN.md section 4 "Outside the megakernel".
  *
  * rt_set_ray_capture arms a capture: every counting render (RT_OPT_DETAIL_COUNTERS)
  * of a W7E3 / W9E1 path mode appends each ray its walks start -- camera, shadow

@@ -114,3 +114,11 @@ def test_capture_stream_equals_render_rays(rt, gpu):
     q = ctx.trace_rays("BSP", rays[camera], None)
     assert set(np.unique(prim_ids)) <= set(np.unique(q["tri"]))
     ctx.close()
+
+
+def test_batch_rejects_2_pow_31_rays(rt, gpu):
+    # k_trace's 2^28-capped shard heads would hand out the same block
+    # forever past 2^31 rays; the ABI refuses such a batch before any launch
+    with pytest.raises(rt._ffi.RtError) as e:
+        gpu.trace_batch("BSP", 256, 256, 1 << 31, 256)   # (the pointers are never read)
+    assert e.value.code == rt._ffi.RT_E_INVALID
