@@ -1311,7 +1311,8 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
         if (c->samples.n < need) HIPCHK(c, c->samples.alloc(need));
         if (async && c->samples2.n < need) HIPCHK(c, c->samples2.alloc(need));
         L.samples = c->samples.as<float4>();
-        const bool autop = sil && c->bsp_cull == RT_BSP_CULL_AUTO && c->hcam_valid;
+        // (a counting render, RT_OPT_DETAIL_COUNTERS, runs other kernels: it never probes)
+        const bool autop = sil && c->bsp_cull == RT_BSP_CULL_AUTO && c->hcam_valid && !c->detail;
         if (autop)
             if (int r = probe_begin(c)) return r;
         if (async) {   // the folds follow the context stream's work up to here

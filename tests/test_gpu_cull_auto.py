@@ -44,6 +44,11 @@ def test_auto_probes_inside_the_render_and_matches_certified(rt):
     ctx.set_option(F.RT_OPT_BSP_CULL, F.RT_BSP_CULL_AUTO)
     assert ctx.bsp_cull_in_use() == (F.RT_BSP_CULL_CERTIFIED, 0.0, 0.0)   # not probed yet: the certified kernel
     assert ctx.bsp_cull_probes() == (0, 0)
+    # a counting render (RT_OPT_DETAIL_COUNTERS: other kernels) does not probe
+    ctx.set_option(F.RT_OPT_DETAIL_COUNTERS, 1)
+    _same(ref[BUNNY_CAM], _render(s, BUNNY_CAM))
+    ctx.set_option(F.RT_OPT_DETAIL_COUNTERS, 0)
+    assert ctx.bsp_cull_probes() == (0, 0)
     # a render too small for a timed launch (4 iterations x 230,400 < 2^20 samples) does not probe
     small = _render(s, BUNNY_CAM, spp=4)
     assert ctx.bsp_cull_probes() == (0, 0)
