@@ -63,6 +63,9 @@ def probe(ctx, rt, wl, trav, W, H, spp, dev, stream, args, chunk):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if args.warm:
                 ctx.render_tiles(wl.mode, trav, r, n, 0, spp, acc.data_ptr(), ids.data_ptr())   # warm
+                # (drained before timing, as the bench drains its warm-up: RT_BSP_CULL_AUTO reads
+                # its probe's events at the next render only once they have completed)
+                torch.cuda.synchronize(dev)
             e0.record(stream)
             ctx.render_tiles(wl.mode, trav, r, n, 0, spp, acc.data_ptr(), ids.data_ptr())
             e1.record(stream)
