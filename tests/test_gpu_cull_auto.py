@@ -174,9 +174,10 @@ def test_held_camera_key_probes_once(rt):
 
     t_cert, f_cert, _, _ = run(F.RT_BSP_CULL_CERTIFIED)
     t_auto, f_auto, probes, used = run(F.RT_BSP_CULL_AUTO)
-    # timing without the frame downloads: best of two runs each
-    t_cert = min(t_cert, run(F.RT_BSP_CULL_CERTIFIED, keep=False)[0])
-    t_auto = min(t_auto, run(F.RT_BSP_CULL_AUTO, keep=False)[0])
+    # timing without the frame downloads: best of three runs each
+    for _ in range(2):
+        t_cert = min(t_cert, run(F.RT_BSP_CULL_CERTIFIED, keep=False)[0])
+        t_auto = min(t_auto, run(F.RT_BSP_CULL_AUTO, keep=False)[0])
     print(f"32 held-key frames: certified {t_cert * 1e3:.1f} ms, auto {t_auto * 1e3:.1f} ms; probes {probes}; "
           f"in use {used}")
     assert probes == (1, 4)
