@@ -1194,7 +1194,7 @@ int rt_bsp_cull_in_use(rt_ctx* c, int* mode, float* probe_ms, uint32_t* probes)
 {
     if (!c || !mode) return RT_E_INVALID;
     if (c->bsp_cull == RT_BSP_CULL_AUTO && c->probe_n == 4 && !c->auto_cull) {
-        if (int r = set_dev(c)) return r;
+        if (int r = set_dev_nojoin(c)) return r;   // (only the event query: no stream work)
         if (int r = probe_finish(c)) return r;
     }
     *mode = (int)cull_in_use(c);
