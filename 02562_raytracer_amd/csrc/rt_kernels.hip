@@ -1385,6 +1385,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(
 k_path(DevScene S, DevLaunch L)
 {
     extern __shared__ uint32_t lds_stack[];   // [level][thread], 4 B entries
+#ifdef RT_DBG_WAVE_TIMES
+    // diagnostic builds only (tools/wave_times.py): each wave's start and end on the
+    // 100-MHz real-time clock, into the ray-capture buffer
+    const uint64_t dbg_t0 = __builtin_amdgcn_s_memrealtime();
+#endif
     // BSP: the lane's column of the [level][thread] stack.  BVH: the wave's
     // column (uniform); a lane adds lane_v() at each access, so no per-lane
     // address stays live across the loop (at 7 waves/SIMD it was spilled;
@@ -1884,6 +1889,15 @@ k_path(DevScene S, DevLaunch L)
         if (__ballot(st != ST_IDLE) == 0) break;
     }
     flush_counters(cnt, L.counters, COUNT);
+#ifdef RT_DBG_WAVE_TIMES
+    if (!COUNT && L.cap_rays && (threadIdx.x & 63u) == 0u) {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        const uint32_t xcc = (uint32_t)__builtin_amdgcn_s_getreg(20 | (0 << 6) | ((4 - 1) << 11));
+        L.cap_rays[blockIdx.x * 4u + (threadIdx.x >> 6)] =
+            make_float4(__uint_as_float((uint32_t)dbg_t0), __uint_as_float((uint32_t)(dbg_t0 >> 32)),
+                        __uint_as_float((uint32_t)t1), __uint_as_float(xcc & 0xFu));
+    }
+#endif
 }
 
 // ------------------------------------------------------------------ progressive fold
