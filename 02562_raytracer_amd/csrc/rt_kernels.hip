@@ -73,6 +73,54 @@ __device__ __forceinline__ uint32_t lane_v()
     return l;
 }
 
+// IEEE-mode v_max / v_min of quiet-NaN-or-number operands.  fmaxf / fminf of
+// a value the compiler cannot prove canonical (a loop-carried tmin / tmax, a
+// kernel argument) get a canonicalising v_max_f32 x, x first -- only a
+// signalling NaN would need it, and no value of the walks is one (every NaN
+// here is produced by arithmetic or is a quiet constant).  The instruction
+// drops a quiet NaN operand exactly as fmaxf / fminf do.  (bsp_box_miss: three
+// such v_max per walking trip.)
+__device__ __forceinline__ float qmax(float a, float b)
+{
+    float r;
+    asm("v_max_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float qmin(float a, float b)
+{
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ float qmax3(float a, float b, float c)
+{
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ __forceinline__ float qmin3(float a, float b, float c)
+{
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// min(x, s) with s a uniform (SGPR) operand
+__device__ __forceinline__ float qmin_s(float s, float x)
+{
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "s"(s), "v"(x));
+    return r;
+}
+// 96 * m (a treelet's byte offset) as two full-rate shifts-and-adds: the
+// compiler's v_mul_lo_u32 is a quarter-rate instruction, and m can exceed the
+// 24 bits of v_mul_u32_u24 (heap indices up to 2^25 at max_depth 24)
+__device__ __forceinline__ uint32_t times96(uint32_t m)
+{
+    uint32_t r;
+    asm("v_lshl_add_u32 %0, %1, 1, %1\n\tv_lshlrev_b32 %0, 5, %0" : "=&v"(r) : "v"(m));
+    return r;
+}
+
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 as_f4(v4u q)
@@ -292,17 +340,36 @@ __device__ __forceinline__ void pixel_uv(const rt_uniform& u, uint32_t x, uint32
 // dist, which becomes tmax; beta and gamma are derived where the hit is shaded
 // (bary_of: the same operations on the same record, so the same bits).  Only
 // an unsettled candidate divides all three quotients.
-template <bool FAST, bool COUNT = false, bool CULL = false, bool BARY = true>
+// VERT: the ray direction is exactly (0, 1, 0) (W9E1's shadow rays,
+// light_init, w9e1.wgsl:67-73, :442-446).  Then cross(ov, w) is (-ov.z, +-0,
+// ov.x) and dot(w, n) is n.y exactly -- each product with 0 is a zero, each
+// with 1 the other operand, and adding a zero changes nothing but the sign of
+// a zero -- so a and b are one product pair and one add each, and the cross
+// product and the denominator cost nothing: 14 arithmetic instructions
+// instead of 32.  Every value equals the general form's except possibly the
+// sign of a zero a, b (or denom, which is then rejected by its magnitude):
+// the predicate below compares them with < / > only, and the sign-bit shortcut
+// of a sure accept falls back to the exact quotients, whose comparisons do not
+// see it either, so the accept decision and dist are the general form's.
+template <bool FAST, bool COUNT = false, bool CULL = false, bool BARY = true, bool VERT = false>
 __device__ __forceinline__ bool tri_math(const float4 r0, const float4 r1, const float4 r2, f3 o, f3 w, float tmin,
-                                         float tmax, float& dist, float& beta, float& gamma, Counters* cn = nullptr)
+                                         float tmax, float& dist, float& beta, float& gamma, Counters* cn = nullptr,
+                                         bool vert = false)
 {
     const f3 v0 = V(r0.x, r0.y, r0.z), e0 = V(r0.w, r1.x, r1.y), e1 = V(r1.z, r1.w, r2.x);
     const f3 n = V(r2.y, r2.z, r2.w);
     const f3 ov = sub(v0, o);
-    const f3 nom = cross(ov, w);
-    const float denom = dot(w, n);
-    const float a = dot(nom, e1);
-    const float b = -dot(nom, e0);
+    float denom, a, b;
+    if (VERT && vert) {
+        denom = n.y;
+        a = (-ov.z) * e1.x + ov.x * e1.z;
+        b = -((-ov.z) * e0.x + ov.x * e0.z);
+    } else {
+        const f3 nom = cross(ov, w);
+        denom = dot(w, n);
+        a = dot(nom, e1);
+        b = -dot(nom, e0);
+    }
     const float c = dot(ov, n);
     bool reject = CULL ? ((rt_absf(denom) < 0.00005f) | (denom > 0.0f)) : rt_absf(denom) < 1e-10f;
     float tq = 0.0f, m = 0.0f, qa = 0.0f, qb = 0.0f, ms = 0.0f;
@@ -468,7 +535,9 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     const float ao = comp(o, axis), iv = comp(inv, axis);
     const uint32_t near_node = 2u * m + (__float_as_uint(iv) >> 31);   // see bsp_inv1
     const float x = __uint_as_float(n.y) - ao;
+#ifndef RT_DBG_VERT
     if (COUNT) c.v[C_EXACT_NODES]++;
+#endif
     const float ad = comp(d, axis);
     const float denom = rt_absf(ad) < 1.0e-8f ? 1.0e-8f : ad;
     // RN(x / denom) from the per-ray RN(1/denom) (include/rt_detmath.h); the IEEE
@@ -516,9 +585,10 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
 // more round trip; loading them with the trip's loads was no faster then,
 // profiles/r03/ab_pre_c*.txt.  The 96-B treelets of the certified culling load
 // them anyway.)
-template <bool COUNT, bool CULL, class LOG>
+template <bool COUNT, bool CULL, class LOG, bool VERT = false>
 __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, const v4u nx, const v4u r1, const v4u q5,
-                                               const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c, LOG& lg)
+                                               const f3 o, const f3 d, bool anyhit, Trav& t, Counters& c, LOG& lg,
+                                               bool vert)
 {
     if ((t.leaf_k != t.leaf_end) & !(anyhit & t.found)) {
         // the trip's 96-B load holds this whole record (nx, r1, r2 = q5)
@@ -529,8 +599,8 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
             c.v[C_TESTS]++;
         }
         float dist, beta, gamma;
-        if (tri_math<true, COUNT, CULL, false>(as_f4(nx), as_f4(r1), as_f4(r2), o, d, t.tmin, t.tmax, dist,
-                                                       beta, gamma, &c)) {
+        if (tri_math<true, COUNT, CULL, false, VERT>(as_f4(nx), as_f4(r1), as_f4(r2), o, d, t.tmin, t.tmax, dist,
+                                                             beta, gamma, &c, vert)) {
             if (COUNT) c.v[C_ACCEPTS]++;
             t.tmax = dist;
             t.found = true;
@@ -544,10 +614,10 @@ __device__ __forceinline__ void leaf_test_next(const __amdgpu_buffer_rsrc_t rs, 
 
 // The leaf half of a BSP trip: test the record in q0..q2 and the next one,
 // whose 48 B are q3..q5.
-template <bool COUNT, bool CULL, class LOG>
+template <bool COUNT, bool CULL, class LOG, bool VERT = false>
 __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, const v4u q0, const v4u q1, const v4u q2,
                                                const v4u q3, const v4u q4, const v4u q5, const f3 o, const f3 d, bool anyhit, Trav& t,
-                                               Counters& c, bool& done, bool& pop, LOG& lg)
+                                               Counters& c, bool& done, bool& pop, LOG& lg, bool vert = false)
 {
     lg.tested(t.leaf_k);
     if (COUNT) {
@@ -555,15 +625,15 @@ __device__ __forceinline__ void bsp_leaf_tests(const __amdgpu_buffer_rsrc_t rs, 
         c.v[C_TESTS]++;
     }
     float dist, beta, gamma;
-    if (tri_math<true, COUNT, CULL, false>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta,
-                                                   gamma, &c)) {
+    if (tri_math<true, COUNT, CULL, false, VERT>(as_f4(q0), as_f4(q1), as_f4(q2), o, d, t.tmin, t.tmax, dist, beta,
+                                                         gamma, &c, vert)) {
         if (COUNT) c.v[C_ACCEPTS]++;
         t.tmax = dist;
         t.found = true;
         t.hit_k = anyhit ? t.hit_k : t.leaf_k;
     }
     t.leaf_k += 48u;
-    leaf_test_next<COUNT, CULL>(rs, q3, q4, q5, o, d, anyhit, t, c, lg);
+    leaf_test_next<COUNT, CULL, LOG, VERT>(rs, q3, q4, q5, o, d, anyhit, t, c, lg, vert);
     const bool leaf_done = (t.leaf_k == t.leaf_end) | (anyhit & t.found);
     done = leaf_done & t.found;   // a leaf with an accepted triangle ends the walk
     pop = leaf_done & !t.found;
@@ -685,22 +755,26 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
         // (fused: fewer roundings than the proof's constants allow for)
         m = __builtin_fmaf(D1, __builtin_fmaf(S.cull_k1 * w1, __builtin_amdgcn_rcpf(den), S.cull_k3), m);
     }
-    float tn = tmin, tf = tmax;
+    float mn[3], mx[3];
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         const float ib = rt_absf(iv[a]) < 1e8f ? iv[a] : iv[a] * __builtin_inff();   // +1e8: a zero component
         const float t1 = (dl[a] - m) * ib, t2 = (dh[a] + m) * ib;
-        tn = __builtin_fmaxf(tn, __builtin_fminf(t1, t2));
-        tf = __builtin_fminf(tf, __builtin_fmaxf(t1, t2));
+        mn[a] = __builtin_fminf(t1, t2);
+        mx[a] = __builtin_fmaxf(t1, t2);
     }
+    // max(tmin, mn...) / min(tmax, mx...) in the order fmaxf / fminf would take
+    // them (qmax: no canonicalising instruction for the loop-carried tmin / tmax)
+    const float tn = qmax(qmax3(tmin, mn[0], mn[1]), mn[2]);
+    const float tf = qmin(qmin3(tmax, mx[0], mx[1]), mx[2]);
     // a clear gap: the rounding of the slab products cannot close it
     // (capped: an infinite slab end from a zero direction component must still
     // show a gap; a finite product cannot reach the cap)
-    const float e = __builtin_fminf((rt_absf(tn) + rt_absf(tf)) * S.bsp_cull_gap, S.bsp_cull_emax);
+    const float e = qmin_s(S.bsp_cull_emax, (rt_absf(tn) + rt_absf(tf)) * S.bsp_cull_gap);
     // the interval the subtree's content can be hit in, widened by the same
     // tolerance (culling off: e = inf or NaN, lo = tmin, hi = tmax)
-    lo = __builtin_fmaxf(tmin, tn - e);
-    hi = __builtin_fminf(tmax, tf + e);
+    lo = qmax(tmin, tn - e);
+    hi = qmin(tmax, tf + e);
     // an empty subtree's content box is +inf / -inf (its slabs are NaN, never a
     // gap): culled outright, except with culling off (e = inf or NaN)
     return (tn - tf > e) | (__uint_as_float(q0.x) - __uint_as_float(q0.w) > e);
@@ -755,7 +829,7 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
     return leaf & !pop;
 }
 
-template <bool COUNT, bool CULL, class LOG, int CM = 1>
+template <bool COUNT, bool CULL, class LOG, int CM = 1, bool VSH = false>
 __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                              bool anyhit, Trav& t, Counters& c, LOG& lg)
 {
@@ -764,7 +838,8 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
     const bool in_leaf = t.leaf_k != t.leaf_end;
     // a leaf lane: its next 96 B of records (two whole records); a walking
     // lane: the 96-B treelet of its node
-    const uint32_t base = in_leaf ? t.leaf_k : t.node * BSP_TREELET_BYTES;
+    static_assert(BSP_TREELET_BYTES == 96, "times96");
+    const uint32_t base = in_leaf ? t.leaf_k : times96(t.node);
     uint64_t tw = COUNT ? __builtin_amdgcn_s_memtime() : 0;
     v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rs, base, 0, 0);
     v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rs, base + 16u, 0, 0);
@@ -797,17 +872,24 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
             c.v[C_MEMWAIT_CYC64] += (uint32_t)(tw >> 6);
     }
     bool done = false, pop = false;
-    if (in_leaf) bsp_leaf_tests<COUNT, CULL>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg);
+    if (in_leaf) {
+        // VSH (W9E1): every any-hit ray is a shadow ray of direction (0, 1, 0).  When
+        // all of the wave's leaf lanes hold one, the wave takes the tests' VERT form
+        // (a uniform branch on a ballot of the any-hit flag; a ballot taken once per
+        // check instead, outside the trips, measured slower: profiles/r06/ab_vsh.txt)
+        bsp_leaf_tests<COUNT, CULL, LOG, VSH>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg,
+                                              VSH && __ballot(!anyhit) == 0);
+    }
     else bsp_walk<COUNT, CM>(S, stk, q0, q1, q2, q3, q4, q5, q6, o, d, inv, t, c, pop);
     if (pop) done = bsp_pop(stk, t);
     return done;
 }
-template <bool COUNT, bool CULL = false, int CM = 1>
+template <bool COUNT, bool CULL = false, int CM = 1, bool VSH = false>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
                                          bool anyhit, Trav& t, Counters& c)
 {
     NoLog lg;
-    return bsp_step_log<COUNT, CULL, NoLog, CM>(S, stk, o, d, inv, anyhit, t, c, lg);
+    return bsp_step_log<COUNT, CULL, NoLog, CM, VSH>(S, stk, o, d, inv, anyhit, t, c, lg);
 }
 
 // RN(1/denom) per axis (denom as bsp.wgsl:63): the approximate interior-node
@@ -1000,13 +1082,13 @@ __device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float
     if (TRAV == RT_TRAVERSE_BVH) bvh_init(t, tmin, tmax);
     else trav_init(t, tmin, tmax);
 }
-template <int TRAV, bool COUNT, bool CULL = false, int CM = 1>
+template <int TRAV, bool COUNT, bool CULL = false, int CM = 1, bool VSH = false>
 __device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const BvhDeep& dp, const f3 o, const f3 d,
                                           const f3 inv, bool anyhit, Trav& t, Counters& c)
 {
     if (TRAV == RT_TRAVERSE_BVH)
         return bvh_step<COUNT, CULL>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv, anyhit, t, c);
-    return bsp_step<COUNT, CULL, CM>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
+    return bsp_step<COUNT, CULL, CM, VSH>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
 }
 
 // Whole traversal of one ray (used by the primary-ray kernel).
@@ -1425,6 +1507,10 @@ k_path(DevScene S, DevLaunch L)
     // walk draws no random numbers, so the PRNG sequence is the reference's, and
     // the direction (3 floats) need not be kept across the walk
     constexpr bool REDRAW = MODE == RT_MODE_W9E1 || MODE == MODE_W9E1_TRANSPARENT;
+    // W9E1: every shadow ray is light_init's (0, 1, 0) (the lambertian branch
+    // below); the BSP walk's leaf tests take their VERT form in the trips whose
+    // leaf lanes all hold one (W9E2 / W9E3 also send other any-hit rays)
+    constexpr bool VSH = REDRAW && TRAV == RT_TRAVERSE_BSP;
     const float ETA = W9 ? 0.0001f : 0.01f;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t T = L.shade_threshold;
@@ -1519,6 +1605,17 @@ k_path(DevScene S, DevLaunch L)
                     cnt.v[C_LANE_STEPS]++;
                     if (leafst) cnt.v[C_LEAF_LANE_STEPS]++;
                 }
+#ifdef RT_DBG_VERT
+                // diagnostic build only: trips whose leaf (walking) lanes are all shadow rays
+                // (C_POPS, unused by the BSP walk; C_EXACT_NODES, whose per-decision count is
+                // C_INTERIOR's)
+                const uint64_t lms = __ballot(st == ST_TRACE && leafst && !shadow);
+                const uint64_t nms = __ballot(st == ST_TRACE && !leafst && !shadow);
+                if (lane == 0) {
+                    cnt.v[C_POPS] += (lm != 0) & (lms == 0);
+                    cnt.v[C_EXACT_NODES] += (nm != 0) & (nms == 0);
+                }
+#endif
                 if (lane == 0) {
                     cnt.v[C_TRIPS]++;
                     cnt.v[C_NODE_TRIPS] += nm != 0;
@@ -1527,7 +1624,7 @@ k_path(DevScene S, DevLaunch L)
             }
             const bool go = st == ST_TRACE;
             if (go) {
-                if (trav_step<TRAV, COUNT, W9E3, CM>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                if (trav_step<TRAV, COUNT, W9E3, CM, VSH>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
             }
             // further steps before the next check: the check (two ballots, a
             // popcount, the compares) is SALU work, and the SALU is a per-CU
@@ -1535,7 +1632,7 @@ k_path(DevScene S, DevLaunch L)
 #pragma unroll
             for (int k = 1; k < (COUNT ? 1 : TRAV == RT_TRAVERSE_BVH ? RT_BVH_TRIPS_PER_CHECK : RT_TRIPS_PER_CHECK); ++k) {
                 if (st == ST_TRACE) {
-                    if (trav_step<TRAV, COUNT, W9E3, CM>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                    if (trav_step<TRAV, COUNT, W9E3, CM, VSH>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
                 }
             }
         }
