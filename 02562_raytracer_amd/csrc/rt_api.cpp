@@ -1111,7 +1111,7 @@ static uint32_t default_threshold(const rt_ctx* c, rt_mode mode, rt_traverse tra
     if (trav == RT_TRAVERSE_BVH) return 4u;
     if (mode == RT_MODE_W7E3) return 24u;
     if (cull == RT_BSP_CULL_SILHOUETTE) return (1u << 16) | (32u << 8) | 24u;
-    return cull_certified(c) ? (1u << 16) | (32u << 8) | 16u : (1u << 16) | (24u << 8) | 8u;
+    return cull_certified(c) ? (1u << 16) | (32u << 8) | 20u : (1u << 16) | (24u << 8) | 8u;
 }
 
 // RT_BSP_CULL_AUTO's probe.  The certified and the silhouette W9E1 kernels are both
@@ -1286,7 +1286,9 @@ static int render_common(rt_ctx* c, rt_mode mode, rt_traverse trav, rtk::DevLaun
     // best, profiles/r03/ab_T{hi,lo}_c{4,5}.txt).  The certified walk visits more
     // nodes and its rays take more trips, so finished lanes wait longer for the last
     // ones: 16 and 32 (profiles/r04/sweep_T.txt: config 3 fixed 16 +1.9 % over 8,
-    // config 4 16..24 +3 %, config 5 32 +1.1 %).
+    // config 4 16..24 +3 %, config 5 32 +1.1 %); 20 and 32 since the cheaper
+    // shadow-ray leaf tests of round 6 (profiles/r06/sweep_T.txt: config 3 +0.3..0.6 %
+    // over 16, config 5 unchanged).
     // The silhouette kernel's camera rays take fewer, dearer trips: 24 and 32
     // (profiles/r05/sweep_T_c4s.txt: config 4 +1.2 % over 16 / 32).
     const bool sil = has_silhouette(c, mode, trav);

@@ -165,7 +165,7 @@ typedef struct rt_ray_counts {
 /* ---- options (rt_set_option) ------------------------------------------- */
 #define RT_OPT_DETAIL_COUNTERS 1  /* 0/1: use the counting kernel instantiation    */
 #define RT_OPT_WAVES_PER_CU    2  /* persistent grid size: waves per CU (default 32; capped by LDS) */
-#define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace; 0 or 64 = all lanes finish their rays first (lockstep); -1 = the default: 24 for W7E3 on the BSP walk, 4 for the BVH walk, and for the other modes on the BSP walk a per-wave choice from the share of its tracing lanes inside a leaf (the higher when >= 1/2): 16 or 32 with certified culling (24 or 32 when the silhouette kernel runs), 8 or 24 otherwise; 0x10000 | hi << 8 | lo sets that choice's two thresholds */
+#define RT_OPT_SHADE_THRESHOLD 3  /* path kernels: shade once <= N of 64 lanes still trace; 0 or 64 = all lanes finish their rays first (lockstep); -1 = the default: 24 for W7E3 on the BSP walk, 4 for the BVH walk, and for the other modes on the BSP walk a per-wave choice from the share of its tracing lanes inside a leaf (the higher when >= 1/2): 20 or 32 with certified culling (24 or 32 when the silhouette kernel runs), 8 or 24 otherwise; 0x10000 | hi << 8 | lo sets that choice's two thresholds */
 #define RT_OPT_SAMPLE_CHUNK    4  /* W7E3/W9E1: progressive iterations per work unit (default 1) */
 #define RT_OPT_SAMPLE_BUDGET_MB 5 /* W7E3/W9E1: device scratch for per-sample results, MiB (default 16384);
                                      a render whose spp x pixels x 16 B exceed it runs in several passes */
