@@ -1120,13 +1120,14 @@ static uint32_t default_threshold(const rt_ctx* c, rt_mode mode, rt_traverse tra
 // configs 3 and 5.  The probe costs no extra work: four of the
 // renders' own launches, each of at least 2^20 samples, run certified, silhouette,
 // certified, silhouette (a big render splits its first iterations into four such
-// launches, 1/16 of it each at most; 1-spp frames of at least 2^20 pixels give one
+// launches, 1/8 of it each at most; 1-spp frames of at least 2^20 pixels give one
 // launch each, so a moving camera's frames finish the probe in four frames).  Their
 // events are read without waiting, at a later render (probe_finish): until then the
 // certified kernel runs.  The choice holds for the scene -- a new BSP, a change of the
 // culling option, or an eye whose reach (farthest distance to the scene box) leaves
 // [1/2, 2] of the reach it was made at starts a new probe; orbiting or small moves keep it.
 static constexpr uint64_t PROBE_MIN_SAMPLES = 1ull << 20;
+static constexpr float PROBE_MARGIN = 0.95f;   // the silhouette kernel's time must be below 0.95x
 
 // the eye's farthest distance to the scene's box (|eye - centre| + half diagonal)
 static float eye_reach(const rt_ctx* c)
@@ -1156,10 +1157,10 @@ static int probe_finish(rt_ctx* c)
     }
     c->auto_ms[0] = best[0];
     c->auto_ms[1] = best[1];
-    // the silhouette kernel must win by 3 %: on config 3 the two probe within 1-4 % of each
-    // other (the certified kernel 4 % faster over whole frames), on config 4 the silhouette
+    // the silhouette kernel must win by 5 %: on config 3 the two probe within 0-4 % of each
+    // other (the certified kernel 4-9 % faster over whole frames), on config 4 the silhouette
     // kernel wins by 8-12 % (profiles/r05/ab_auto.txt, the final bench lines' bsp_cull)
-    c->auto_cull = best[1] < 0.97f * best[0] ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
+    c->auto_cull = best[1] < PROBE_MARGIN * best[0] ? RT_BSP_CULL_SILHOUETTE : RT_BSP_CULL_CERTIFIED;
     return RT_OK;
 }
 
@@ -1185,8 +1186,14 @@ static uint32_t probe_take(const rt_ctx* c, uint32_t n, uint32_t total, uint32_t
     if (c->auto_cull || c->probe_n >= 4 || stride == 0) return 0;
     const uint64_t need = (PROBE_MIN_SAMPLES + stride - 1) / stride;
     if (n < need) return 0;
-    const uint64_t cap = std::max<uint64_t>(1, (1ull << 25) / stride);
-    const uint64_t want = std::max<uint64_t>(need, std::min<uint64_t>(total / 16, cap));
+    // (an eighth of the render each, at most 2^26 samples: a launch's fixed ~1.3-ms tail
+    //  must stay small against the launch, or the two kernels' tails
+    // decide the choice -- with 1/16 and 2^25, rank 0's share of a 4-rank config-3 split
+    // probed the silhouette kernel 3.7 % faster in 3.6-ms launches, and it ran the frame
+    // 8.6 % slower than the certified one, profiles/r06/final/bench_c3n4.json of fatbin
+    // 104178909346469f)
+    const uint64_t cap = std::max<uint64_t>(1, (1ull << 26) / stride);
+    const uint64_t want = std::max<uint64_t>(need, std::min<uint64_t>(total / 8, cap));
     return (uint32_t)std::min<uint64_t>(n, want);
 }
 

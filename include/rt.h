@@ -208,10 +208,11 @@ typedef struct rt_ray_counts {
 #define RT_BSP_CULL_AUTO       4  /* (default) exact as RT_BSP_CULL_CERTIFIED: the W9E1 BSP renders time the
                                      certified and the silhouette kernels on four of their own launches (certified,
                                      silhouette, certified, silhouette; each at least 2^20 samples: a big render
-                                     splits its first iterations, 1-spp frames give one launch each), with no extra
+                                     splits its first iterations, up to an eighth of it or 2^26 samples per
+                                     launch, 1-spp frames give one launch each), with no extra
                                      work and no host wait (the events are read at a later render; the certified
                                      kernel runs until then), and run the faster from then on (the silhouette
-                                     kernel must be 3 % faster to be chosen), until the BSP or this option changes
+                                     kernel must be 5 % faster to be chosen), until the BSP or this option changes
                                      or the eye's reach (farthest distance to the scene box) leaves [1/2, 2] of the
                                      reach the probe ran at.  rt_bsp_cull_in_use reports the choice */
 
