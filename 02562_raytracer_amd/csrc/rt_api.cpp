@@ -74,6 +74,7 @@ struct rt_ctx {
     uint32_t unit_order = 1;            // 0: chunk-major, 1: pixel-major
     uint32_t bsp_cull = RT_BSP_CULL_AUTO;   // RT_OPT_BSP_CULL: subtree culling by content boxes in the BSP walk
     float bsp_scale = 0.0f;             // the scene's coordinate magnitude (set on upload; the margins' scale)
+    uint32_t bsp_div_checked = 1;       // DevScene.bsp_div_checked (launch_plane_range, on upload)
     uint64_t sample_budget_mb = 16384;  // per-sample scratch (one pass at 1080p x 256 spp needs 8.1 GiB)
     DevBuf samples;
     bool detail = false;
@@ -85,6 +86,7 @@ struct rt_ctx {
     DevBuf pos, nrm, idx, mats, lights;
     DevBuf bsp_nodes, bsp_ids;   // bsp_nodes: [8-B nodes | 48-B records]
     DevBuf bsp_tm;               // per record slot {triangle id, material} (DevScene.bsp_tm)
+    DevBuf plane_flag;           // launch_plane_range's 4-B result
     DevBuf bsp_ref_tree, bsp_ref_planes;   // bsp_array + planes in the reference layout (rt_download_bsp)
     float bsp_aabb8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     uint32_t bsp_nnodes = 0, bsp_nids = 0;
@@ -543,7 +545,14 @@ static int repack_bsp(rt_ctx* c, uint32_t nnodes, uint32_t nids, size_t rec_off,
                                (uint32_t)rec_off, c->bsp_nodes.p, c->pos.as<float4>(), c->idx.as<uint4>(),
                                c->bsp_ids.as<uint32_t>(), nids, 0.0f, boxes.p, c->bsp_tm.as<uint2>(), c->stream))
         return fail(c, RT_E_DEVICE, "BSP repack launch failed");
+    if (!c->plane_flag.p) HIPCHK(c, c->plane_flag.alloc(4));
+    if (rtk::launch_plane_range(c->bsp_ref_tree.as<uint32_t>(), c->bsp_ref_planes.as<float>(), nnodes,
+                                c->plane_flag.as<uint32_t>(), c->stream))
+        return fail(c, RT_E_DEVICE, "BSP plane range launch failed");
+    uint32_t pflag = 1;
+    HIPCHK(c, hipMemcpyAsync(&pflag, c->plane_flag.p, 4, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->bsp_div_checked = pflag != 0u;
     float scale = 0.0f;
     for (int k : {0, 1, 2, 4, 5, 6})
         if (std::isfinite(aabb[k])) scale = std::max(scale, std::fabs(aabb[k]));
@@ -997,6 +1006,7 @@ static rtk::DevScene dev_scene(const rt_ctx* c)
     S.bsp_tm = c->bsp_tm.as<uint2>();
     S.bsp_sil = c->bsp_sil.as<uint4>();
     S.bsp_cull_mode = cull_in_use(c);
+    S.bsp_div_checked = c->bsp_div_checked;
     S.bsp_depth = c->bsp_depth;
     memcpy(S.aabb, c->aabb, sizeof S.aabb);
     S.bvh_base = c->bvh_nodes.as<uint8_t>();

@@ -777,6 +777,32 @@ int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, 
     return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
 }
 
+// Whether the walk's plane divisions need their range check (rt_kernels.hip bsp_decide):
+// rt_div_by_recip is exact for x = plane - o with x == 0 or 2^-100 <= |x| <= 2^100
+// (include/rt_detmath.h).  That holds for every ray origin coordinate o that is 0 or
+// in [2^-76, 2^99] in magnitude (k_path checks those per ray) when every interior
+// plane is too: the difference of two such floats is 0, or a nonzero multiple of
+// 2^-99, or at most 2^100.  flag |= 1 for a plane outside that range.
+__global__ void __launch_bounds__(256) k_plane_range(const uint32_t* tree, const float* planes, uint32_t nnodes,
+                                                     uint32_t* flag)
+{
+    bool out = false;
+    for (size_t i = (size_t)blockIdx.x * 256u + threadIdx.x; i < nnodes; i += (size_t)gridDim.x * 256u) {
+        if ((tree[4 * i] & 3u) == 3u) continue;   // a leaf: no plane
+        const float a = fabsf(planes[i]);
+        out |= !(a == 0.0f || (a >= 0x1p-76f && a <= 0x1p99f));
+    }
+    if (__ballot(out) != 0 && (threadIdx.x & 63u) == 0u) atomicOr(flag, 1u);
+}
+
+int launch_plane_range(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t* flag, hipStream_t s)
+{
+    if (hipMemsetAsync(flag, 0, 4, s) != hipSuccess) return RT_E_DEVICE;
+    const uint32_t g = std::max<uint32_t>(1, std::min<uint32_t>(4096, (nnodes + 255) / 256));
+    hipLaunchKernelGGL(k_plane_range, dim3(g), dim3(256), 0, s, tree, planes, nnodes, flag);
+    return hipGetLastError() == hipSuccess ? 0 : RT_E_DEVICE;
+}
+
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
                       const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,
                       void* box_scratch, uint2* tm, hipStream_t s)

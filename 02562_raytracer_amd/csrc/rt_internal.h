@@ -64,6 +64,9 @@ struct DevScene {
     // triangles' normals and the rest's term, 16 B at [M] (rt_bsp_build.hip k_treelet_hcam)
     const uint4* bsp_sil;
     uint32_t bsp_cull_mode;   // RT_BSP_CULL_* (the host picks k_path's instantiation by it)
+    // 1: some interior plane lies outside {0} U [2^-76, 2^99] in magnitude, so the walk's
+    // divisions keep their per-decision range check for every ray (launch_plane_range)
+    uint32_t bsp_div_checked;
 };
 
 // Work mapping + outputs of one launch.
@@ -165,6 +168,8 @@ constexpr uint32_t BSP_TREELET_BYTES = 96;
 // silhouette data for RT_BSP_CULL_SILHOUETTE (sil: (nnodes + 1) x 16 B; scratch: nnodes x 24 B)
 int launch_bsp_camera(const uint32_t* tree, uint32_t nnodes, const float4* pos, const uint4* idx, const uint32_t* ids,
                       uint32_t nids, const float eye[3], void* blob, uint32_t* sil, void* scratch, hipStream_t stream);
+// flag (device, 4 B) = 1 when an interior plane lies outside {0} U [2^-76, 2^99] in magnitude
+int launch_plane_range(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t* flag, hipStream_t stream);
 // tm: nids x {triangle id, material} in treeIds order (or null)
 int launch_bsp_repack(const uint32_t* tree, const float* planes, uint32_t nnodes, uint32_t rec_off, void* blob,
                       const float4* pos, const uint4* idx, const uint32_t* ids, uint32_t nids, float margin,

@@ -526,9 +526,20 @@ __device__ __forceinline__ bool bsp_pop(const float* stk, Trav& t)
 // this level's slot), and sets the trail bit with one shift-or.  Every decision
 // divides out the exact t (the wave runs the exact path in nearly every trip
 // anyway: 28 % of decisions need it), with no approximate test first.
+// chk (wave-uniform, k_path's per-check choice): some lane's ray, or the scene's planes
+// (rt_bsp_build.hip k_plane_range), may put x outside the range where rt_div_by_recip
+// is exact.  Without it every x is 0 or inside the range (x = +-0 gives a zero, whose
+// sign may differ from x / denom's for -0: t values are only compared, and every
+// comparison sees +0 == -0, tests/native/fastdiv_check.c), so the per-lane test and its
+// fallback branch are skipped: a scalar
+// branch instead of three VALU and about five scalar instructions per decision, and
+// scalar issue costs the trip as much as vector issue does (profiles/r06/ab_chk.txt;
+// two instantiations of the whole trip group instead, one per value, ran 5 % slower:
+// twice the code and more spills)
 template <bool COUNT>
 __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32_t m, uint32_t dep, const f3 o,
-                                               const f3 d, const f3 inv, Trav& t, Counters& c, float lo, float& hi)
+                                               const f3 d, const f3 inv, Trav& t, Counters& c, float lo, float& hi,
+                                               uint32_t chk = 1u)
 {
     if (COUNT) c.v[C_INTERIOR]++;
     const uint32_t axis = n.x & 3u;
@@ -543,9 +554,11 @@ __device__ __forceinline__ uint32_t bsp_decide(float* stk, const uint2 n, uint32
     // RN(x / denom) from the per-ray RN(1/denom) (include/rt_detmath.h); the IEEE
     // division outside its operand range or for a NaN-flagged axis
     float tt = rt_div_by_recip(x, denom, iv);
-    if (!(rt_div_by_recip_ok(x) & (iv == iv))) {
-        asm volatile("");   // keep the rare IEEE division behind its branch (no if-conversion)
-        tt = x / denom;
+    if (chk != 0u) {
+        if (!(rt_div_by_recip_ok(x) & (iv == iv))) {
+            asm volatile("");   // keep the rare IEEE division behind its branch (no if-conversion)
+            tt = x / denom;
+        }
     }
     // against [lo, hi]: the ray interval, clipped to the treelet root's content
     // box (bsp_box_miss); a plane beyond it leaves one side hitless
@@ -790,7 +803,7 @@ __device__ __forceinline__ bool bsp_box_miss(const DevScene& S, const v4u q0, co
 template <bool COUNT, int CM = 1>
 __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4u q0, const v4u q1, const v4u q2,
                                          const v4u q3, const v4u q4, const v4u q5, const v4u q6, const f3 o, const f3 d,
-                                         const f3 inv, Trav& t, Counters& c, bool& pop)
+                                         const f3 inv, Trav& t, Counters& c, bool& pop, uint32_t chk = 1u)
 {
     uint32_t m = t.node;
     float lo = t.tmin, hi = t.tmax;   // the decisions' interval: [tmin, tmax] clipped to the box
@@ -808,15 +821,15 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
     if (!leaf) {
         // the trail slot of this level
         float* const s0 = stk + dep * 256u;
-        m = bsp_decide<COUNT>(s0, n, m, dep, o, d, inv, t, c, lo, hi);
+        m = bsp_decide<COUNT>(s0, n, m, dep, o, d, inv, t, c, lo, hi, chk);
         n = (m & 1u) ? make_uint2(q2.z, q2.w) : make_uint2(q2.x, q2.y);
         leaf = (n.x & 3u) == 3u;
         if (!leaf) {
-            m = bsp_decide<COUNT>(s0 + 256, n, m, dep + 1u, o, d, inv, t, c, lo, hi);
+            m = bsp_decide<COUNT>(s0 + 256, n, m, dep + 1u, o, d, inv, t, c, lo, hi, chk);
             const v4u g = (m & 2u) ? q4 : q3;
             n = (m & 1u) ? make_uint2(g.z, g.w) : make_uint2(g.x, g.y);
             leaf = (n.x & 3u) == 3u;
-            if (!leaf) m = bsp_decide<COUNT>(s0 + 512, n, m, dep + 2u, o, d, inv, t, c, lo, hi);
+            if (!leaf) m = bsp_decide<COUNT>(s0 + 512, n, m, dep + 2u, o, d, inv, t, c, lo, hi, chk);
         }
     }
     t.node = m;
@@ -831,7 +844,7 @@ __device__ __forceinline__ bool bsp_walk(const DevScene& S, float* stk, const v4
 
 template <bool COUNT, bool CULL, class LOG, int CM = 1, bool VSH = false>
 __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
-                                             bool anyhit, Trav& t, Counters& c, LOG& lg)
+                                             bool anyhit, Trav& t, Counters& c, LOG& lg, uint32_t chk = 1u)
 {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc((void*)S.bsp_nodes, (short)0, (int)S.bsp_bytes, 0x00020000);
@@ -880,16 +893,16 @@ __device__ __forceinline__ bool bsp_step_log(const DevScene& S, float* stk, cons
         bsp_leaf_tests<COUNT, CULL, LOG, VSH>(rs, q0, q1, q2, q3, q4, q5, o, d, anyhit, t, c, done, pop, lg,
                                               VSH && __ballot(!anyhit) == 0);
     }
-    else bsp_walk<COUNT, CM>(S, stk, q0, q1, q2, q3, q4, q5, q6, o, d, inv, t, c, pop);
+    else bsp_walk<COUNT, CM>(S, stk, q0, q1, q2, q3, q4, q5, q6, o, d, inv, t, c, pop, chk);
     if (pop) done = bsp_pop(stk, t);
     return done;
 }
 template <bool COUNT, bool CULL = false, int CM = 1, bool VSH = false>
 __device__ __forceinline__ bool bsp_step(const DevScene& S, float* stk, const f3 o, const f3 d, const f3 inv,
-                                         bool anyhit, Trav& t, Counters& c)
+                                         bool anyhit, Trav& t, Counters& c, uint32_t chk = 1u)
 {
     NoLog lg;
-    return bsp_step_log<COUNT, CULL, NoLog, CM, VSH>(S, stk, o, d, inv, anyhit, t, c, lg);
+    return bsp_step_log<COUNT, CULL, NoLog, CM, VSH>(S, stk, o, d, inv, anyhit, t, c, lg, chk);
 }
 
 // RN(1/denom) per axis (denom as bsp.wgsl:63): the approximate interior-node
@@ -1084,11 +1097,11 @@ __device__ __forceinline__ void trav_start(Trav& t, void* stk, float tmin, float
 }
 template <int TRAV, bool COUNT, bool CULL = false, int CM = 1, bool VSH = false>
 __device__ __forceinline__ bool trav_step(const DevScene& S, void* stk, const BvhDeep& dp, const f3 o, const f3 d,
-                                          const f3 inv, bool anyhit, Trav& t, Counters& c)
+                                          const f3 inv, bool anyhit, Trav& t, Counters& c, uint32_t chk = 1u)
 {
     if (TRAV == RT_TRAVERSE_BVH)
         return bvh_step<COUNT, CULL>(S, reinterpret_cast<uint32_t*>(stk), dp, o, d, inv, anyhit, t, c);
-    return bsp_step<COUNT, CULL, CM, VSH>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c);
+    return bsp_step<COUNT, CULL, CM, VSH>(S, reinterpret_cast<float*>(stk), o, d, inv, anyhit, t, c, chk);
 }
 
 // Whole traversal of one ray (used by the primary-ray kernel).
@@ -1622,9 +1635,24 @@ k_path(DevScene S, DevLaunch L)
                     cnt.v[C_LEAF_TRIPS] += lm != 0;
                 }
             }
+            // the plane divisions' range check (bsp_decide): kept for the next trips when
+            // the scene's planes need it or a tracing lane's ray has a direction component
+            // of magnitude <= 1e-8 other than 0 (a NaN in inv) or an origin coordinate
+            // outside {0} U [2^-76, 2^99] in magnitude; no lane starts a new ray before the
+            // next check
+            uint32_t chk = 1u;
+            if (TRAV == RT_TRAVERSE_BSP) {
+                const float ax = rt_absf(ro.x), ay = rt_absf(ro.y), az = rt_absf(ro.z);
+                const float isum = inv.x + inv.y + inv.z;   // |inv| <= 1e8: NaN only from a flag
+                const bool odd = (isum != isum) | (((ax < 0x1p-76f) & (ax != 0.0f)) | (ax > 0x1p99f)) |
+                                 (((ay < 0x1p-76f) & (ay != 0.0f)) | (ay > 0x1p99f)) |
+                                 (((az < 0x1p-76f) & (az != 0.0f)) | (az > 0x1p99f));
+                // (readfirstlane: a wave-uniform scalar)
+                chk = __builtin_amdgcn_readfirstlane((S.bsp_div_checked != 0u || __ballot((st == ST_TRACE) & odd) != 0) ? 1u : 0u);
+            }
             const bool go = st == ST_TRACE;
             if (go) {
-                if (trav_step<TRAV, COUNT, W9E3, CM, VSH>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                if (trav_step<TRAV, COUNT, W9E3, CM, VSH>(S, stk, dp, ro, rd, inv, shadow, tr, cnt, chk)) st = ST_SHADE;
             }
             // further steps before the next check: the check (two ballots, a
             // popcount, the compares) is SALU work, and the SALU is a per-CU
@@ -1632,7 +1660,7 @@ k_path(DevScene S, DevLaunch L)
 #pragma unroll
             for (int k = 1; k < (COUNT ? 1 : TRAV == RT_TRAVERSE_BVH ? RT_BVH_TRIPS_PER_CHECK : RT_TRIPS_PER_CHECK); ++k) {
                 if (st == ST_TRACE) {
-                    if (trav_step<TRAV, COUNT, W9E3, CM, VSH>(S, stk, dp, ro, rd, inv, shadow, tr, cnt)) st = ST_SHADE;
+                    if (trav_step<TRAV, COUNT, W9E3, CM, VSH>(S, stk, dp, ro, rd, inv, shadow, tr, cnt, chk)) st = ST_SHADE;
                 }
             }
         }
